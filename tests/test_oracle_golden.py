@@ -1,0 +1,90 @@
+"""Pin the CPU oracle (oracle/admm_oracle.py) to the reference's golden fixtures.
+
+The fixtures were captured from the reference itself (tests/golden/make_golden.py).
+The oracle keeps the reference's op structure, so in one process on the CPU it
+must reproduce them BIT-EXACTLY: weights, losses, line-search decisions and their
+operands, and the full primal/dual state.
+"""
+import pytest
+import torch
+
+from golden_io import ALL, FULL, GATES6, WEIGHT_NAMES, Golden
+from oracle import admm_oracle as O
+
+FAST = [n for n in ALL if not n.startswith('t1_')] + ['t1_gstock']
+
+
+def _run(g: Golden, steps=None):
+    torch.manual_seed(0)
+    W = O.init_weights(g.D, g.H, g.O)
+    st = O.init_state(g.x, g.y, W)
+    stp = O.Stepper(O.Hyper.from_dict(g.params, g.variant, g.with_dual_y))
+    for s in range(1, (steps or g.steps) + 1):
+        rec = stp.step(st)
+        yield s, st, rec
+
+
+@pytest.mark.parametrize('name', ALL)
+def test_seeded_init_matches(name):
+    g = Golden(name)
+    torch.manual_seed(0)
+    W = O.init_weights(g.D, g.H, g.O)
+    for k in WEIGHT_NAMES:
+        assert torch.equal(W[k], g.t(f'w0_{k}')), k
+    assert O.mse(g.x, g.y, W) == g.losses[0]
+
+
+@pytest.mark.parametrize('name', FULL)
+def test_initial_state_matches(name):
+    g = Golden(name)
+    st = O.init_state(g.x, g.y, g.weights(0))
+    S, L = g.state(0)
+    for q in GATES6:
+        assert torch.equal(st.S[q], S[q]), q
+        assert torch.equal(st.L[q], L[q]), q
+    assert torch.equal(st.S['a'], S['a'])
+
+
+@pytest.mark.parametrize('name', FAST)
+def test_trajectory_bit_exact(name):
+    g = Golden(name)
+    for s, st, rec in _run(g, steps=min(g.steps, 8)):
+        assert [r['k'] for r in rec['weights']] == g.ks(s), f'step {s}'
+        for r, ref in zip(rec['weights'], g.searches[s - 1]['weights']):
+            assert [(a, b, w) for a, b, w in r['tests']] == [tuple(v) for v in ref]
+        assert [tuple(v) for v in g.searches[s - 1]['hT']] == [tuple(v) for v in rec['hT']['tests']]
+        for k in WEIGHT_NAMES:
+            assert torch.equal(st.W[k], g.t(f'w{s}_{k}')), (s, k)
+        assert O.mse(g.x, g.y, st.W) == g.losses[s]
+        if g.full_state:
+            S, L = g.state(s)
+            for q in GATES6:
+                assert torch.equal(st.S[q], S[q]), (s, q)
+                assert torch.equal(st.L[q], L[q]), (s, q)
+            assert torch.equal(st.S['a'], S['a'])
+            assert torch.equal(st.L['y'], L['y'])
+
+
+@pytest.mark.parametrize('name', FULL)
+def test_teacher_forced_step(name):
+    """From the reference's state after step k, one oracle step gives its state after k+1."""
+    g = Golden(name)
+    stp = O.Stepper(O.Hyper.from_dict(g.params, g.variant, g.with_dual_y))
+    for k in range(g.steps):
+        S, L = g.state(k)
+        st = O.State(g.x, g.y, g.weights(k), S, L, g.B)
+        stp.step(st)
+        S1, L1 = g.state(k + 1)
+        for q in GATES6:
+            assert torch.equal(st.S[q], S1[q]) and torch.equal(st.L[q], L1[q]), (k, q)
+        for n in WEIGHT_NAMES:
+            assert torch.equal(st.W[n], g.t(f'w{k + 1}_{n}')), (k, n)
+
+
+def test_dead_searches_are_dead():
+    """The wy and c searches never iterate in the reference: pinned by the capture."""
+    for name in ALL:
+        g = Golden(name)
+        for rec in g.searches:
+            assert rec['wy_true'] == 0 and rec['c_true'] == 0
+            assert rec['c_count'] == g.T

@@ -1,0 +1,156 @@
+// admm_dev.hpp -- device-side building blocks for the gfx950 ADMM-LSTM step.
+//
+//  * activation numerics shared by every kernel (so that a gate stored as phi(z) and a
+//    residual recomputed from the same z agree bit-for-bit: step 1 of the reference has
+//    exactly zero weight gradients, admm.py:302-312 with gates == phi(z));
+//  * accurate increments phi(z+d) - phi(z) for the line-search trials (no cancellation
+//    at tiny d, see DESIGN.md "line-search numerics");
+//  * an fp32 MFMA tile engine (v_mfma_f32_32x32x2_f32, exact f32 products/sums) with
+//    LDS staging, used by the time-step GEMM, the Q = A*G GEMM and the A^T*R reduction.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace admm {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+constexpr int kWave = 64;
+constexpr int kThreads = 256;  // every kernel: 4 waves per workgroup
+
+// ----------------------------------------------------------------------------- numerics
+
+struct SigPair {
+  float s;   // sigma(z)
+  float sc;  // 1 - sigma(z), computed without cancellation
+};
+
+__device__ __forceinline__ SigPair sig_pair(float z) {
+  const float e = expf(-fabsf(z));
+  const float r = 1.0f / (1.0f + e);
+  const float er = e * r;
+  return z >= 0.f ? SigPair{r, er} : SigPair{er, r};
+}
+
+__device__ __forceinline__ float sigm(float z) { return sig_pair(z).s; }
+
+__device__ __forceinline__ float act(bool is_tanh, float z) { return is_tanh ? tanhf(z) : sigm(z); }
+
+// 1/cosh(x) without overflow
+__device__ __forceinline__ float sech(float x) {
+  const float u = expf(-fabsf(x));
+  return 2.0f * u / (1.0f + u * u);
+}
+
+// sigma(z+d) - sigma(z) = sigma(z+d) * (1 - sigma(z)) * (1 - e^{-d}); every factor is
+// computed without cancellation, so the increment is accurate to a few ulp for all d.
+__device__ __forceinline__ float dsigmoid(float z, float d, float s, float sc) {
+  if (fabsf(d) >= 16.f) return sigm(z + d) - s;
+  return sigm(z + d) * sc * (-expm1f(-d));
+}
+
+// tanh(z+d) - tanh(z) = sinh(d) * sech(z+d) * sech(z)
+__device__ __forceinline__ float dtanh(float z, float d, float u, float sz) {
+  if (fabsf(d) >= 16.f) return tanhf(z + d) - u;
+  return sinhf(d) * sech(z + d) * sz;
+}
+
+// ----------------------------------------------------------------------------- reductions
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, kWave);
+  return v;
+}
+
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, kWave);
+  return v;
+}
+
+// Deterministic block sum of one value per thread (fixed tree), result valid in thread 0.
+template <typename T>
+__device__ __forceinline__ T block_sum(T v, T* red /* >= 4 entries of LDS */) {
+  v = wave_sum(v);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  if (lane == 0) red[w] = v;
+  __syncthreads();
+  T r = 0;
+  if (threadIdx.x == 0) r = (red[0] + red[1]) + (red[2] + red[3]);
+  __syncthreads();
+  return r;
+}
+
+// ----------------------------------------------------------------------------- MFMA tile engine
+//
+// C[BM x BN] += A[BM x K] * B[K x BN], K streamed in chunks of KC through LDS.
+// Waves are laid out (BM/WM) x (BN/WN) (must be 4); each wave owns (WM/32) x (WN/32)
+// 32x32 accumulators.  Fragment maps of v_mfma_f32_32x32x2_f32 (gfx950):
+//   A: lane l holds A[i = l&31][k = l>>5];  B: B[k = l>>5][j = l&31];
+//   C/D register r: row = (r&3) + 8*(r>>2) + 4*(l>>5), col = l&31.
+// The operand source P provides a(m, k) and b(k, n) global loads (returning 0 outside the
+// problem) and A_M_FAST (which index is contiguous in memory, for coalesced staging).
+
+template <int BM, int BN, int WM, int WN>
+struct TileShape {
+  static constexpr int KC = 16;
+  static constexpr int MT = WM / 32, NT = WN / 32;
+  static constexpr int WAVES_N = BN / WN;
+  static_assert((BM / WM) * (BN / WN) == 4, "4 waves per workgroup");
+  static constexpr int A_STRIDE = KC + 1;  // +1 dword: conflict-free ds_read_b32 down a column
+  static constexpr int LDS_FLOATS = BM * A_STRIDE + KC * BN;
+};
+
+__device__ __forceinline__ int acc_row(int r, int lane) { return (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5); }
+
+template <int BM, int BN, int WM, int WN, class P>
+__device__ __forceinline__ void gemm_tile(const P& p, int64_t m0, int64_t n0, int64_t k0, int64_t k1,
+                                          f32x16 (&acc)[WM / 32][WN / 32], float* smem) {
+  using S = TileShape<BM, BN, WM, WN>;
+  constexpr int KC = S::KC;
+  float* As = smem;
+  float* Bs = smem + BM * S::A_STRIDE;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm0 = (wave / S::WAVES_N) * WM, wn0 = (wave % S::WAVES_N) * WN;
+
+  for (int64_t kb = k0; kb < k1; kb += KC) {
+    const int kn = (int)((k1 - kb) < KC ? (k1 - kb) : KC);
+    for (int i = tid; i < BM * KC; i += kThreads) {
+      int m, k;
+      if (P::A_M_FAST) { m = i % BM; k = i / BM; } else { k = i % KC; m = i / KC; }
+      As[m * S::A_STRIDE + k] = (k < kn) ? p.a(m0 + m, kb + k) : 0.f;
+    }
+    for (int i = tid; i < KC * BN; i += kThreads) {
+      const int n = i % BN, k = i / BN;
+      Bs[k * BN + n] = (k < kn) ? p.b(kb + k, n0 + n) : 0.f;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int kk = 0; kk < KC; kk += 2) {
+      float av[S::MT], bv[S::NT];
+#pragma unroll
+      for (int mi = 0; mi < S::MT; ++mi) av[mi] = As[(wm0 + mi * 32 + (lane & 31)) * S::A_STRIDE + kk + (lane >> 5)];
+#pragma unroll
+      for (int ni = 0; ni < S::NT; ++ni) bv[ni] = Bs[(kk + (lane >> 5)) * BN + wn0 + ni * 32 + (lane & 31)];
+#pragma unroll
+      for (int mi = 0; mi < S::MT; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < S::NT; ++ni)
+          acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[mi], bv[ni], acc[mi][ni], 0, 0, 0);
+    }
+    __syncthreads();
+  }
+}
+
+template <int MT, int NT>
+__device__ __forceinline__ void zero_acc(f32x16 (&acc)[MT][NT]) {
+#pragma unroll
+  for (int mi = 0; mi < MT; ++mi)
+#pragma unroll
+    for (int ni = 0; ni < NT; ++ni)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[mi][ni][r] = 0.f;
+}
+
+}  // namespace admm

@@ -1,0 +1,456 @@
+// admm_host.hip -- context, step orchestration and the C ABI of libadmmlstm.so
+// (include/admm_lstm.h).  Everything is enqueued on the caller's stream; no host sync
+// except admm_get_stats.  Multi-GPU: one process per GPU, the batch sums of the step are
+// all-reduced with RCCL (the only cross-sample couplings of the reference).
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+
+#include "admm_kernels.hpp"
+#include "admm_lstm.h"
+
+using namespace admm;
+
+namespace {
+
+thread_local std::string g_last_error;
+
+int fail(int code, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  g_last_error = buf;
+  return code;
+}
+
+#define HIP_TRY(expr)                                                                             \
+  do {                                                                                            \
+    hipError_t e_ = (expr);                                                                       \
+    if (e_ != hipSuccess) return fail(ADMM_EHIP, "%s failed: %s", #expr, hipGetErrorString(e_)); \
+  } while (0)
+
+#define NCCL_TRY(expr)                                                                              \
+  do {                                                                                              \
+    ncclResult_t r_ = (expr);                                                                       \
+    if (r_ != ncclSuccess) return fail(ADMM_ECOMM, "%s failed: %s", #expr, ncclGetErrorString(r_)); \
+  } while (0)
+
+template <typename T>
+int dalloc(T** p, size_t n) {
+  *p = nullptr;
+  if (n == 0) n = 1;
+  hipError_t e = hipMalloc((void**)p, n * sizeof(T));
+  if (e != hipSuccess) return fail(ADMM_ENOMEM, "hipMalloc(%zu bytes) failed: %s", n * sizeof(T), hipGetErrorString(e));
+  return ADMM_OK;
+}
+
+}  // namespace
+
+struct AdmmCtx {
+  Geom g{};
+  Hyper hp{};
+  int device = 0;
+  AdmmBuffers buf{};
+  bool bound = false;
+  bool z_valid = false;
+  int steps = 0;
+  // workspace (all device)
+  float *zc = nullptr, *tgt = nullptr, *R = nullptr, *Q = nullptr;  // [4][BT][H]
+  float *G = nullptr, *dW = nullptr, *gslab = nullptr;
+  int nsplit_max = 1;
+  double *fw_part = nullptr, *tr_part = nullptr, *tr_sums = nullptr;
+  int nblk_resid = 1, nblk_trial = 1;
+  int* found = nullptr;
+  float *U = nullptr, *wy_slab = nullptr, *Gy = nullptr;
+  int wy_nsplit = 1;
+  double *ht_part = nullptr, *ht_sums = nullptr;
+  int ht_nblk = 1;
+  DevStats* stats = nullptr;
+  // multi-GPU
+  ncclComm_t comm = nullptr;
+  int rank = 0, world = 1;
+};
+
+namespace {
+
+Weights weights_of(const AdmmCtx* c) {
+  Weights w;
+  for (int q = 0; q < 4; ++q) {
+    w.wx[q] = c->buf.wx[q];
+    w.wh[q] = c->buf.wh[q];
+  }
+  return w;
+}
+
+Planes6 planes(float* const p[6]) {
+  Planes6 r;
+  for (int i = 0; i < 6; ++i) r.p[i] = p[i];
+  return r;
+}
+
+int allreduce_f32(AdmmCtx* c, float* p, size_t n, hipStream_t s) {
+  if (c->world <= 1) return ADMM_OK;
+  NCCL_TRY(ncclAllReduce(p, p, n, ncclFloat32, ncclSum, c->comm, s));
+  return ADMM_OK;
+}
+
+int allreduce_f64(AdmmCtx* c, double* p, size_t n, hipStream_t s) {
+  if (c->world <= 1) return ADMM_OK;
+  NCCL_TRY(ncclAllReduce(p, p, n, ncclFloat64, ncclSum, c->comm, s));
+  return ADMM_OK;
+}
+
+// wy update (admm.py:246-280; admm.no_dual_y.py:226-249)
+int stage_wy(AdmmCtx* c, hipStream_t s) {
+  const Geom& g = c->g;
+  launch_wy_grad(g, c->hp, c->buf.gates[ADMM_H], c->buf.a, c->buf.dual_y, c->buf.wy, c->U, c->wy_slab,
+                 c->wy_nsplit, s);
+  launch_wy_reduce(g, c->wy_slab, c->wy_nsplit, c->Gy, s);
+  int rc = allreduce_f32(c, c->Gy, (size_t)g.H * g.O, s);
+  if (rc) return rc;
+  launch_wy_apply(g, c->hp, c->Gy, c->buf.wy, s);
+  return ADMM_OK;
+}
+
+// One weight stage: the 4 gates' (side) weights, each a backtracking proximal-linearised
+// update (admm.py:282-343).  side 0 = x2q (input weights), side 1 = h2q (recurrent).
+int stage_weights(AdmmCtx* c, int side, hipStream_t s) {
+  const Geom& g = c->g;
+  const int Kd = side == 0 ? g.D : g.H;
+  HIP_TRY(hipMemsetAsync(c->found, 0, 4 * sizeof(int), s));
+  ResidArgs ra{};
+  ra.stage = side;
+  ra.x = c->buf.x;
+  ra.S = planes(c->buf.gates);
+  ra.L = planes(c->buf.duals);
+  ra.zc = c->zc;
+  ra.tgt = c->tgt;
+  ra.R = c->R;
+  ra.dW = c->dW;
+  ra.fw_part = c->fw_part;
+  ra.nblk = c->nblk_resid;
+  launch_resid(g, c->hp, ra, s);
+  const int ns = atr_splits(g, side);
+  launch_atr(g, side, c->buf.x, c->buf.gates[ADMM_H], c->R, c->gslab, ns, s);
+  launch_reduce_g(g, side, c->hp, c->gslab, ns, c->G, s);
+  int rc = allreduce_f32(c, c->G, (size_t)4 * Kd * g.H, s);
+  if (rc) return rc;
+  launch_qgemm(g, side, c->buf.x, c->buf.gates[ADMM_H], c->G, c->Q, s);
+  SelectArgs sa{};
+  sa.side = side;
+  sa.last_pass = kMaxPasses - 1;
+  sa.sums = c->tr_sums;
+  sa.G = c->G;
+  for (int q = 0; q < 4; ++q) sa.W[q] = side == 0 ? c->buf.wx[q] : c->buf.wh[q];
+  sa.dW = side == 0 ? c->dW : nullptr;
+  sa.found = c->found;
+  sa.stats = c->stats;
+  for (int pass = 0; pass < kMaxPasses; ++pass) {
+    launch_trial(g, pass, c->zc, c->tgt, c->Q, c->found, c->tr_part, c->nblk_trial, s);
+    launch_trial_reduce(g, pass, c->tr_part, c->nblk_trial, c->fw_part, c->nblk_resid, c->found, c->tr_sums, s);
+    rc = allreduce_f64(c, c->tr_sums, 4 * (kTrialJ + 1), s);
+    if (rc) return rc;
+    sa.pass = pass;
+    launch_select(g, c->hp, sa, s);
+  }
+  return ADMM_OK;
+}
+
+// Sequential sweep t = 1..T (admm.py:72-76) and the h_T / a / dual work at T.
+int stage_sweep(AdmmCtx* c, hipStream_t s) {
+  const Geom& g = c->g;
+  const Weights w = weights_of(c);
+  SweepT sa{};
+  sa.x = c->buf.x;
+  sa.S = planes(c->buf.gates);
+  sa.L = planes(c->buf.duals);
+  sa.zc = c->zc;
+  for (int t = 1; t <= g.T; ++t) launch_sweep_t(g, t, w, c->hp, sa, s);
+  launch_ht_partial(g, c->hp, sa.S, sa.L, c->buf.a, c->buf.dual_y, c->buf.wy, c->ht_part, c->ht_nblk, s);
+  launch_ht_reduce(c->ht_part, c->ht_nblk, c->ht_sums, s);
+  int rc = allreduce_f64(c, c->ht_sums, kHTSums, s);
+  if (rc) return rc;
+  launch_ht_apply(g, c->hp, sa.S, sa.L, c->buf.a, c->buf.dual_y, c->buf.y, c->buf.wy, c->ht_sums, c->stats, s);
+  return ADMM_OK;
+}
+
+int check_dims(const AdmmDims* d) {
+  if (!d) return fail(ADMM_EINVAL, "dims is NULL");
+  if (d->batch <= 0 || d->seq_len <= 0 || d->input_size <= 0 || d->hidden_size <= 0 || d->output_size <= 0)
+    return fail(ADMM_EINVAL, "all dims must be positive (B=%lld T=%d D=%d H=%d O=%d)", (long long)d->batch,
+                d->seq_len, d->input_size, d->hidden_size, d->output_size);
+  if (d->global_batch < d->batch) return fail(ADMM_EINVAL, "global_batch < batch");
+  if (d->output_size > 8) return fail(ADMM_EINVAL, "output_size %d > 8 is not supported", d->output_size);
+  return ADMM_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int32_t admm_abi_version(void) { return ADMM_LSTM_ABI_VERSION; }
+
+const char* admm_build_info(void) {
+  return "libadmmlstm gfx950 (fp32 MFMA v_mfma_f32_32x32x2_f32, RCCL), abi " "1";
+}
+
+const char* admm_last_error(void) { return g_last_error.c_str(); }
+
+int admm_create(const AdmmDims* dims, const AdmmParams* params, int device, AdmmCtx** out) {
+  if (!out) return fail(ADMM_EINVAL, "out is NULL");
+  *out = nullptr;
+  int rc = check_dims(dims);
+  if (rc) return rc;
+  if (!params) return fail(ADMM_EINVAL, "params is NULL");
+  if (params->variant != ADMM_VARIANT_ADMM && params->variant != ADMM_VARIANT_NO_DUAL_Y)
+    return fail(ADMM_EINVAL, "unknown variant %d", params->variant);
+  for (int i = 0; i < 7; ++i)
+    if (!std::isfinite(params->rho[i])) return fail(ADMM_EINVAL, "rho[%d] is not finite", i);
+  HIP_TRY(hipSetDevice(device));
+  AdmmCtx* c = new AdmmCtx();
+  c->device = device;
+  Geom& g = c->g;
+  g.B = dims->batch;
+  g.Bg = dims->global_batch;
+  g.T = dims->seq_len;
+  g.D = dims->input_size;
+  g.H = dims->hidden_size;
+  g.O = dims->output_size;
+  Hyper& h = c->hp;
+  for (int i = 0; i < 7; ++i) h.rho[i] = params->rho[i];
+  for (int q = 0; q < 4; ++q) {
+    h.beta_x[q] = params->beta_x[q];
+    h.beta_h[q] = params->beta_h[q];
+  }
+  h.beta_y = params->beta_y;
+  h.variant = params->variant;
+  h.with_dual_y = params->with_dual_y;
+
+  const size_t plane = (size_t)g.BT() * g.H;
+  const int Kmax = g.D > g.H ? g.D : g.H;
+  c->nblk_resid = resid_blocks(g);
+  c->nblk_trial = trial_blocks(g);
+  c->nsplit_max = atr_splits(g, 0) > atr_splits(g, 1) ? atr_splits(g, 0) : atr_splits(g, 1);
+  c->wy_nsplit = wy_splits(g);
+  c->ht_nblk = ht_blocks(g);
+  if ((rc = dalloc(&c->zc, 4 * plane)) || (rc = dalloc(&c->tgt, 4 * plane)) || (rc = dalloc(&c->R, 4 * plane)) ||
+      (rc = dalloc(&c->Q, 4 * plane)) || (rc = dalloc(&c->G, (size_t)4 * Kmax * g.H)) ||
+      (rc = dalloc(&c->dW, (size_t)4 * g.D * g.H)) ||
+      (rc = dalloc(&c->gslab, (size_t)c->nsplit_max * 4 * Kmax * g.H)) ||
+      (rc = dalloc(&c->fw_part, (size_t)4 * c->nblk_resid)) ||
+      (rc = dalloc(&c->tr_part, (size_t)4 * kTrialJ * c->nblk_trial)) ||
+      (rc = dalloc(&c->tr_sums, (size_t)4 * (kTrialJ + 1))) || (rc = dalloc(&c->found, 4)) ||
+      (rc = dalloc(&c->U, (size_t)g.B * g.O)) || (rc = dalloc(&c->wy_slab, (size_t)c->wy_nsplit * g.H * g.O)) ||
+      (rc = dalloc(&c->Gy, (size_t)g.H * g.O)) || (rc = dalloc(&c->ht_part, (size_t)c->ht_nblk * kHTSums)) ||
+      (rc = dalloc(&c->ht_sums, kHTSums)) || (rc = dalloc(&c->stats, 1))) {
+    std::string msg = g_last_error;
+    admm_destroy(c);
+    return fail(rc, "%s", msg.c_str());
+  }
+  if (hipMemset(c->stats, 0, sizeof(DevStats)) != hipSuccess) {
+    admm_destroy(c);
+    return fail(ADMM_EHIP, "hipMemset(stats) failed");
+  }
+  *out = c;
+  return ADMM_OK;
+}
+
+int admm_destroy(AdmmCtx* c) {
+  if (!c) return ADMM_OK;
+  (void)hipSetDevice(c->device);
+  void* ptrs[] = {c->zc, c->tgt, c->R, c->Q, c->G, c->dW, c->gslab, c->fw_part, c->tr_part, c->tr_sums, c->found,
+                  c->U, c->wy_slab, c->Gy, c->ht_part, c->ht_sums, c->stats};
+  for (void* p : ptrs)
+    if (p) (void)hipFree(p);
+  if (c->comm) ncclCommDestroy(c->comm);
+  delete c;
+  return ADMM_OK;
+}
+
+int admm_bind(AdmmCtx* c, const AdmmBuffers* b) {
+  if (!c || !b) return fail(ADMM_EINVAL, "NULL argument");
+  const void* req[] = {b->x, b->y, b->wy, b->a, b->dual_y};
+  for (const void* p : req)
+    if (!p) return fail(ADMM_EINVAL, "admm_bind: a required buffer is NULL");
+  for (int q = 0; q < 4; ++q)
+    if (!b->wx[q] || !b->wh[q]) return fail(ADMM_EINVAL, "admm_bind: weight %d is NULL", q);
+  for (int q = 0; q < 6; ++q)
+    if (!b->gates[q] || !b->duals[q]) return fail(ADMM_EINVAL, "admm_bind: gate/dual %d is NULL", q);
+  c->buf = *b;
+  c->bound = true;
+  c->z_valid = false;
+  return ADMM_OK;
+}
+
+int admm_set_with_dual_y(AdmmCtx* c, int32_t flag) {
+  if (!c) return fail(ADMM_EINVAL, "NULL ctx");
+  c->hp.with_dual_y = flag ? 1 : 0;
+  return ADMM_OK;
+}
+
+int admm_invalidate_cache(AdmmCtx* c) {
+  if (!c) return fail(ADMM_EINVAL, "NULL ctx");
+  c->z_valid = false;
+  return ADMM_OK;
+}
+
+int admm_init_state(AdmmCtx* c, void* stream) {
+  if (!c) return fail(ADMM_EINVAL, "NULL ctx");
+  if (!c->bound) return fail(ADMM_ESTATE, "admm_init_state before admm_bind");
+  hipStream_t s = (hipStream_t)stream;
+  const Geom& g = c->g;
+  HIP_TRY(hipSetDevice(c->device));
+  const size_t pbytes = (size_t)g.B * g.TP() * g.H * sizeof(float);
+  for (int q = 0; q < 6; ++q) {
+    HIP_TRY(hipMemsetAsync(c->buf.gates[q], 0, pbytes, s));
+    HIP_TRY(hipMemsetAsync(c->buf.duals[q], 0, pbytes, s));
+  }
+  HIP_TRY(hipMemsetAsync(c->buf.dual_y, 0, (size_t)g.B * g.O * sizeof(float), s));
+  const Weights w = weights_of(c);
+  const int64_t rs = (int64_t)g.TP() * g.H;
+  for (int t = 1; t <= g.T; ++t) {
+    ForwardT fa{};
+    fa.x = c->buf.x;
+    fa.hprev = c->buf.gates[ADMM_H] + (int64_t)(t - 1) * g.H;
+    fa.hprev_stride = rs;
+    fa.cprev = c->buf.gates[ADMM_C] + (int64_t)(t - 1) * g.H;
+    fa.cprev_stride = rs;
+    fa.hout = c->buf.gates[ADMM_H] + (int64_t)t * g.H;
+    fa.hout_stride = rs;
+    fa.cout = c->buf.gates[ADMM_C] + (int64_t)t * g.H;
+    fa.cout_stride = rs;
+    for (int q = 0; q < 4; ++q) fa.gout[q] = c->buf.gates[q] + (int64_t)t * g.H;
+    fa.gout_stride = rs;
+    fa.zc = c->zc;
+    launch_forward_t(g, t, w, fa, s);
+  }
+  launch_rowdot(g.B, g.H, g.O, c->buf.gates[ADMM_H] + (int64_t)g.T * g.H, rs, c->buf.wy, c->buf.a, s);
+  HIP_TRY(hipGetLastError());
+  c->z_valid = true;
+  return ADMM_OK;
+}
+
+int admm_step(AdmmCtx* c, void* stream) {
+  if (!c) return fail(ADMM_EINVAL, "NULL ctx");
+  if (!c->bound) return fail(ADMM_ESTATE, "admm_step before admm_bind");
+  hipStream_t s = (hipStream_t)stream;
+  HIP_TRY(hipSetDevice(c->device));
+  int rc;
+  if (!c->z_valid) launch_zgemm(c->g, weights_of(c), c->buf.x, c->buf.gates[ADMM_H], c->zc, s);
+  if ((rc = stage_wy(c, s))) return rc;
+  if ((rc = stage_weights(c, 0, s))) return rc;
+  if ((rc = stage_weights(c, 1, s))) return rc;
+  if ((rc = stage_sweep(c, s))) return rc;
+  HIP_TRY(hipGetLastError());
+  c->z_valid = true;  // the sweep left x_t Wx + h_{t-1} Wh of the final state in the cache
+  c->steps++;
+  return ADMM_OK;
+}
+
+int admm_comm_unique_id(void* out, int64_t out_bytes) {
+  if (!out || out_bytes < (int64_t)sizeof(ncclUniqueId)) return fail(ADMM_EINVAL, "unique id buffer too small");
+  ncclUniqueId id;
+  NCCL_TRY(ncclGetUniqueId(&id));
+  std::memcpy(out, &id, sizeof id);
+  return ADMM_OK;
+}
+
+int admm_set_comm(AdmmCtx* c, const void* uid, int64_t id_bytes, int rank, int world) {
+  if (!c || !uid || id_bytes < (int64_t)sizeof(ncclUniqueId)) return fail(ADMM_EINVAL, "bad arguments");
+  if (world < 1 || rank < 0 || rank >= world) return fail(ADMM_EINVAL, "bad rank %d / world %d", rank, world);
+  HIP_TRY(hipSetDevice(c->device));
+  if (c->comm) {
+    ncclCommDestroy(c->comm);
+    c->comm = nullptr;
+  }
+  c->rank = rank;
+  c->world = world;
+  if (world == 1) return ADMM_OK;
+  ncclUniqueId id;
+  std::memcpy(&id, uid, sizeof id);
+  NCCL_TRY(ncclCommInitRank(&c->comm, world, id, rank));
+  return ADMM_OK;
+}
+
+int admm_get_stats(AdmmCtx* c, AdmmStats* out) {
+  if (!c || !out) return fail(ADMM_EINVAL, "NULL argument");
+  HIP_TRY(hipSetDevice(c->device));
+  DevStats d;
+  HIP_TRY(hipDeviceSynchronize());
+  HIP_TRY(hipMemcpy(&d, c->stats, sizeof d, hipMemcpyDeviceToHost));
+  std::memset(out, 0, sizeof *out);
+  out->steps = c->steps;
+  for (int i = 0; i < 8; ++i) {
+    out->k[i] = d.k[i];
+    out->f_w[i] = d.f_w[i];
+    out->grad_sq[i] = d.grad_sq[i];
+  }
+  out->passes[0] = d.passes[0];
+  out->passes[1] = d.passes[1];
+  out->theta_h = d.theta_h;
+  out->unresolved = d.unresolved;
+  out->nonfinite = d.nonfinite;
+  return ADMM_OK;
+}
+
+int admm_forward(const float* x, int64_t batch, int32_t seq_len, int32_t input_size, int32_t hidden_size,
+                 int32_t output_size, const float* const wx[4], const float* const wh[4], const float* wy,
+                 float* const gates_out[6], float* h_scratch, float* c_scratch, float* z_out, float* out_a,
+                 void* stream) {
+  AdmmDims d{batch, batch, seq_len, input_size, hidden_size, output_size};
+  int rc = check_dims(&d);
+  if (rc) return rc;
+  if (!x || !wy || !out_a) return fail(ADMM_EINVAL, "admm_forward: NULL buffer");
+  if (!gates_out && (!h_scratch || !c_scratch)) return fail(ADMM_EINVAL, "admm_forward: need gates_out or scratch");
+  hipStream_t s = (hipStream_t)stream;
+  Geom g{batch, batch, seq_len, input_size, hidden_size, output_size};
+  Weights w;
+  for (int q = 0; q < 4; ++q) {
+    if (!wx[q] || !wh[q]) return fail(ADMM_EINVAL, "admm_forward: NULL weight");
+    w.wx[q] = wx[q];
+    w.wh[q] = wh[q];
+  }
+  const int64_t BH = batch * (int64_t)hidden_size;
+  if (!gates_out) {  // gates_out: time-0 slices are the caller's initial c/h (blocks/lstm.py:69-72)
+    HIP_TRY(hipMemsetAsync(h_scratch, 0, (size_t)BH * sizeof(float), s));
+    HIP_TRY(hipMemsetAsync(c_scratch, 0, (size_t)BH * sizeof(float), s));
+  }
+  const int64_t rs = (int64_t)(seq_len + 1) * hidden_size;
+  for (int t = 1; t <= seq_len; ++t) {
+    ForwardT fa{};
+    fa.x = x;
+    if (gates_out) {
+      fa.hprev = gates_out[ADMM_H] + (int64_t)(t - 1) * hidden_size;
+      fa.cprev = gates_out[ADMM_C] + (int64_t)(t - 1) * hidden_size;
+      fa.hout = gates_out[ADMM_H] + (int64_t)t * hidden_size;
+      fa.cout = gates_out[ADMM_C] + (int64_t)t * hidden_size;
+      fa.hprev_stride = fa.cprev_stride = fa.hout_stride = fa.cout_stride = rs;
+      for (int q = 0; q < 4; ++q) fa.gout[q] = gates_out[q] + (int64_t)t * hidden_size;
+      fa.gout_stride = rs;
+    } else {
+      fa.hprev = h_scratch + ((t - 1) & 1) * BH;
+      fa.cprev = c_scratch + ((t - 1) & 1) * BH;
+      fa.hout = h_scratch + (t & 1) * BH;
+      fa.cout = c_scratch + (t & 1) * BH;
+      fa.hprev_stride = fa.cprev_stride = fa.hout_stride = fa.cout_stride = hidden_size;
+    }
+    fa.zc = z_out;
+    launch_forward_t(g, t, w, fa, s);
+  }
+  if (gates_out)
+    launch_rowdot(batch, hidden_size, output_size, gates_out[ADMM_H] + (int64_t)seq_len * hidden_size, rs, wy, out_a,
+                  s);
+  else
+    launch_rowdot(batch, hidden_size, output_size, h_scratch + (seq_len & 1) * BH, hidden_size, wy, out_a, s);
+  HIP_TRY(hipGetLastError());
+  return ADMM_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,135 @@
+// admm_kernels.hpp -- launch interface between the host orchestration (admm_host.hip)
+// and the gfx950 kernels (admm_kernels.hip).  Plain pointers only.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace admm {
+
+constexpr int kTrialJ = 16;      // line-search candidates evaluated per trial pass
+constexpr int kMaxPasses = 4;    // => exponents k in [0, 64)
+constexpr int kHTCand = 4;       // theta = 0.1, 0.2, 0.4, 0.8 (admm.py:447-480)
+constexpr int kHTSums = 1 + 3 * kHTCand;
+
+struct Geom {
+  int64_t B;    // local rows
+  int64_t Bg;   // global rows (a-update constant)
+  int T, D, H, O;
+  __host__ __device__ int64_t BT() const { return B * (int64_t)T; }
+  __host__ __device__ int TP() const { return T + 1; }
+};
+
+struct Weights {            // model parameters, read in place (no packing)
+  const float* wx[4];
+  const float* wh[4];
+};
+
+struct Planes6 { float* p[6]; };
+
+struct Hyper {
+  float rho[7];             // i f g o c h y
+  float beta_x[4], beta_h[4], beta_y;
+  int variant;              // 0 admm, 1 no_dual_y
+  int with_dual_y;
+};
+
+// Device-side diagnostics, copied out by admm_get_stats.
+struct DevStats {
+  int k[8];
+  int passes[2];
+  int unresolved;
+  int nonfinite;
+  float theta_h;
+  int pad;
+  double f_w[8];
+  double grad_sq[8];
+};
+
+// ---- time step (one t): GEMM [x_t | h_{t-1}] @ [Wx; Wh] for the 4 gates + fused epilogue
+struct ForwardT {
+  const float* x;           // [B,T,D]
+  const float* hprev; int64_t hprev_stride;   // row b of h_{t-1} at hprev + b*stride
+  const float* cprev; int64_t cprev_stride;
+  float* hout; int64_t hout_stride;
+  float* cout; int64_t cout_stride;
+  float* gout[4]; int64_t gout_stride;        // i,f,g,o at t (nullable)
+  float* zc;                                  // [4][B*T][H] (nullable)
+};
+void launch_forward_t(const Geom& g, int t, const Weights& w, const ForwardT& a, hipStream_t s);
+
+struct SweepT {
+  const float* x;
+  Planes6 S, L;             // [B,T+1,H] each
+  float* zc;                // [4][B*T][H]: z cache for the next step's first weight stage
+};
+void launch_sweep_t(const Geom& g, int t, const Weights& w, const Hyper& hp, const SweepT& a, hipStream_t s);
+
+// out[b][o] = h_row(b) . wy[:, o]
+void launch_rowdot(int64_t B, int H, int O, const float* h, int64_t h_stride, const float* wy, float* out,
+                   hipStream_t s);
+
+// ---- weight stage (4 gates at once)
+// z cache recompute over all rows: zc[q] = X Wx_q + Hprev Wh_q
+void launch_zgemm(const Geom& g, const Weights& w, const float* x, const float* Sh, float* zc, hipStream_t s);
+
+struct ResidArgs {
+  int stage;                // 0 = x side, 1 = h side
+  const float* x;
+  Planes6 S, L;
+  float* zc;                // read (stage 0) / read-modify-write (stage 1: += X dWx)
+  float* tgt;               // written (stage 0) / read (stage 1); [4][BT][H] = L/rho + S
+  float* R;                 // [4][BT][H] residual (phi(z) - tgt) * phi'(z)
+  const float* dW;          // [4][D][H] (stage 1)
+  double* fw_part;          // [4][nblk]
+  int nblk;
+};
+int resid_blocks(const Geom& g);
+void launch_resid(const Geom& g, const Hyper& hp, const ResidArgs& a, hipStream_t s);
+
+// Gslab[split][q][m][j] = sum_{rows in split} A[row][m] * R[q][row][j], A = X (side 0) or Hprev (side 1)
+int atr_splits(const Geom& g, int side);
+void launch_atr(const Geom& g, int side, const float* x, const float* Sh, const float* R, float* Gslab,
+                int nsplit, hipStream_t s);
+// G[q][m][j] = rho_q * sum_split Gslab
+void launch_reduce_g(const Geom& g, int side, const Hyper& hp, const float* Gslab, int nsplit, float* G,
+                     hipStream_t s);
+// Q[q][row][j] = sum_m A[row][m] * G[q][m][j]
+void launch_qgemm(const Geom& g, int side, const float* x, const float* Sh, const float* G, float* Q,
+                  hipStream_t s);
+
+// trial pass: part[q][jj][blk] = sum over elements of inc(k = pass*J + jj)
+int trial_blocks(const Geom& g);
+void launch_trial(const Geom& g, int pass, const float* zc, const float* tgt, const float* Q, const int* found,
+                  double* part, int nblk, hipStream_t s);
+// sums[q][0..J) = sum_blk part ; sums[q][J] = f(W) partial sum
+void launch_trial_reduce(const Geom& g, int pass, const double* part, int nblk, const double* fw_part,
+                         int fw_nblk, const int* found, double* sums, hipStream_t s);
+// decide the first passing k in this pass's window; on success update the weights
+struct SelectArgs {
+  int side;                 // 0 x, 1 h
+  int pass, last_pass;
+  const double* sums;       // [4][J+1]
+  const float* G;           // [4][K][H]
+  float* W[4];              // weights being updated (in place)
+  float* dW;                // [4][K][H] W_new - W_old (side 0), nullable
+  int* found;
+  DevStats* stats;
+};
+void launch_select(const Geom& g, const Hyper& hp, const SelectArgs& a, hipStream_t s);
+
+// ---- output weight wy (admm.py:246-280; admm.no_dual_y.py:226-249)
+int wy_splits(const Geom& g);
+void launch_wy_grad(const Geom& g, const Hyper& hp, const float* Sh, const float* a, const float* Ly,
+                    const float* wy, float* U, float* slab, int nsplit, hipStream_t s);
+void launch_wy_reduce(const Geom& g, const float* slab, int nsplit, float* Gy, hipStream_t s);
+void launch_wy_apply(const Geom& g, const Hyper& hp, const float* Gy, float* wy, hipStream_t s);
+
+// ---- h_T search (admm.py:459-487; admm.no_dual_y.py:426-449), a update, duals at T
+int ht_blocks(const Geom& g);
+void launch_ht_partial(const Geom& g, const Hyper& hp, const Planes6& S, const Planes6& L, const float* a,
+                       const float* Ly, const float* wy, double* part, int nblk, hipStream_t s);
+void launch_ht_reduce(const double* part, int nblk, double* sums, hipStream_t s);
+void launch_ht_apply(const Geom& g, const Hyper& hp, const Planes6& S, const Planes6& L, float* a, float* Ly,
+                     const float* y, const float* wy, const double* sums, DevStats* stats, hipStream_t s);
+
+}  // namespace admm

@@ -1,0 +1,152 @@
+/*
+ * admm_lstm.h -- C ABI of libadmmlstm.so, the MI355X (gfx950) implementation of the
+ * ADMM-LSTM update step of Frederick2309/ADMM-LSTM.
+ *
+ * The reference has no FFI of its own: its hot path is the Python method
+ * ADMMBasedOptimizer.step() (admm.py:62-78; variant admm.no_dual_y.py:52-66) and
+ * the model-side forward LSTM.init_gate_variables / LSTM.forward
+ * (blocks/lstm.py:43-46, 65-88).  Each entry point below replaces one of those
+ * Python calls; the Python drop-in (admm-lstm_amd/admm.py) binds them with ctypes
+ * exactly as shown in INTEGRATION.md.
+ *
+ * Conventions
+ *  - Plain C types only: device pointers (float*), sizes, a hipStream_t passed as void*.
+ *  - Every function returns 0 on success and a negative ADMM_E* code on failure;
+ *    admm_last_error() returns the thread-local message of the last failure.
+ *  - Enqueue-only: admm_step / admm_init_state / admm_forward never synchronise the
+ *    host with the device; results are stream-ordered on the given stream.
+ *  - Buffers are BORROWED: the caller (PyTorch) owns them, keeps them alive and
+ *    contiguous, and re-binds (admm_bind) whenever a pointer changes.
+ *  - Layouts are the reference's: x [B,T,D], y [B,O], gates/duals [B,T+1,H]
+ *    (time index 0 = the zero initial state), weights x2q [D,H], h2q [H,H], out [H,O].
+ *  - One context per (process, device).  Calls on one context are not thread-safe.
+ */
+#ifndef ADMM_LSTM_H
+#define ADMM_LSTM_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ADMM_LSTM_ABI_VERSION 1
+
+enum {
+  ADMM_OK = 0,
+  ADMM_EINVAL = -1,   /* bad argument / shape / parameter */
+  ADMM_EHIP = -2,     /* HIP runtime error */
+  ADMM_ENOMEM = -3,   /* device allocation failed */
+  ADMM_ECOMM = -4,    /* RCCL error */
+  ADMM_ESTATE = -5    /* call not valid in the context's state (e.g. step before bind) */
+};
+
+enum { ADMM_VARIANT_ADMM = 0, ADMM_VARIANT_NO_DUAL_Y = 1 };
+
+/* Gate order everywhere: i, f, g, o, c, h (admm.py:170; blocks/lstm.py:86-88). */
+enum { ADMM_I = 0, ADMM_F = 1, ADMM_G = 2, ADMM_O = 3, ADMM_C = 4, ADMM_H = 5 };
+
+typedef struct AdmmDims {
+  int64_t batch;          /* rows held by this rank (train_x.size(0) of the shard) */
+  int64_t global_batch;   /* rows over all ranks: the B of the a-update, admm.py:496-502 */
+  int32_t seq_len;        /* T */
+  int32_t input_size;     /* D */
+  int32_t hidden_size;    /* H */
+  int32_t output_size;    /* O */
+} AdmmDims;
+
+typedef struct AdmmParams {
+  /* rho i,f,g,o,c,h,y   (parameters.py 'rho'; admm.py:148-162) */
+  float rho[7];
+  /* beta for x2i,x2f,x2g,x2o ('wi','wf','wg','wo') and h2i..h2o ('vi'..'vo'), and wy
+     (parameters.py 'beta'; admm.py:126-146) */
+  float beta_x[4];
+  float beta_h[4];
+  float beta_y;
+  int32_t variant;        /* ADMM_VARIANT_ADMM (admm.py) or ADMM_VARIANT_NO_DUAL_Y (admm.no_dual_y.py) */
+  int32_t with_dual_y;    /* module flag admm.with_dual_y (admm.py:12); admm variant only */
+} AdmmParams;
+
+typedef struct AdmmBuffers {
+  const float* x;         /* [B,T,D] train_x shard */
+  const float* y;         /* [B,O]   train_y shard */
+  float* wx[4];           /* model.x2i .. x2o  [D,H] */
+  float* wh[4];           /* model.h2i .. h2o  [H,H] */
+  float* wy;              /* model.out [H,O] */
+  float* gates[6];        /* optimizer.gates['i'..'h'] [B,T+1,H] */
+  float* duals[6];        /* optimizer.duals['i'..'h'] [B,T+1,H] */
+  float* a;               /* optimizer.gates['a'] [B,O] */
+  float* dual_y;          /* optimizer.duals['y'] [B,O] */
+} AdmmBuffers;
+
+/* Per-step diagnostics (admm_get_stats; the only call that synchronises). */
+typedef struct AdmmStats {
+  int32_t steps;              /* steps run on this context */
+  int32_t k[8];               /* chosen line-search exponent of the last step, order
+                                 (x,i),(h,i),(x,f),(h,f),(x,g),(h,g),(x,o),(h,o) (admm.py:69-71):
+                                 theta* = 2^k / 2 (admm.py:331-338) */
+  int32_t passes[2];          /* trial passes used by the x and h stage searches */
+  double f_w[8];              /* objective f(W) of each weight search (admm.py:316-325) */
+  double grad_sq[8];          /* ||G||^2 of each weight search */
+  float theta_h;              /* theta* of the h_T search (admm.py:474-482) */
+  int32_t unresolved;         /* weight searches that hit the candidate cap (should be 0) */
+  int32_t nonfinite;          /* NaN/Inf seen in line-search sums (should be 0) */
+} AdmmStats;
+
+typedef struct AdmmCtx AdmmCtx;
+
+/* ABI version (ADMM_LSTM_ABI_VERSION) and the gfx arch the library was built for. */
+int32_t admm_abi_version(void);
+const char* admm_build_info(void);
+const char* admm_last_error(void);
+
+/* ADMMBasedOptimizer.__init__ (admm.py:34-60): validates dims/params, allocates the
+   device workspace (z cache, residual/trial scratch, packed weights). */
+int admm_create(const AdmmDims* dims, const AdmmParams* params, int device, AdmmCtx** out);
+int admm_destroy(AdmmCtx* ctx);
+
+/* Point the context at the caller-owned tensors (admm.py:45-60 attributes). Invalidates
+   the z cache. */
+int admm_bind(AdmmCtx* ctx, const AdmmBuffers* bufs);
+
+/* Replaces admm.py:164-173 (__initialize_primal_gates / __initialize_dual_variables):
+   gates <- LSTM forward of x (blocks/lstm.py:65-88), a <- h_T @ out, duals <- 0. */
+int admm_init_state(AdmmCtx* ctx, void* stream);
+
+/* Replaces ADMMBasedOptimizer.step() (admm.py:62-78 / admm.no_dual_y.py:52-66). */
+int admm_step(AdmmCtx* ctx, void* stream);
+
+/* The module flag admm.with_dual_y is read at every step in the reference (admm.py:77,
+   255, 461, 498); the drop-in forwards its current value before each admm_step. */
+int admm_set_with_dual_y(AdmmCtx* ctx, int32_t flag);
+
+/* The z cache (x_t Wx + h_{t-1} Wh for every t, produced by the time sweep) is reused by
+   the next step's first weight stage.  Call after modifying weights/gates/x outside
+   admm_step; the next step then recomputes it. */
+int admm_invalidate_cache(AdmmCtx* ctx);
+
+/* Multi-GPU (one process per GPU): rank 0 calls admm_comm_unique_id, the bytes are
+   broadcast out of band (torch.distributed), every rank calls admm_set_comm.  All batch
+   sums of the step are then all-reduced with RCCL over xGMI. */
+int admm_comm_unique_id(void* out, int64_t out_bytes);
+int admm_set_comm(AdmmCtx* ctx, const void* unique_id, int64_t id_bytes, int rank, int world);
+
+int admm_get_stats(AdmmCtx* ctx, AdmmStats* out);
+
+/* LSTM.forward / init_gate_variables (blocks/lstm.py:43-46, 65-88) without a context.
+   x [B,T,D]; wx/wh/wy as above; out_a [B,O].  If gates_out is non-NULL it holds six
+   [B,T+1,H] tensors that receive i,f,g,o,c,h at t >= 1 (their time-0 slices are the
+   initial state and are read, not written: zero them, or pass c/h as the reference
+   does, blocks/lstm.py:69-72); otherwise h_scratch and
+   c_scratch ([2,B,H] each) are used.  z_out (may be NULL) receives [4,B*T,H] pre-activations. */
+int admm_forward(const float* x, int64_t batch, int32_t seq_len, int32_t input_size,
+                 int32_t hidden_size, int32_t output_size,
+                 const float* const wx[4], const float* const wh[4], const float* wy,
+                 float* const gates_out[6], float* h_scratch, float* c_scratch,
+                 float* z_out, float* out_a, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* ADMM_LSTM_H */

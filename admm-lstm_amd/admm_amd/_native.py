@@ -25,6 +25,10 @@ ABI_VERSION = 1
 VARIANT_ADMM, VARIANT_NO_DUAL_Y = 0, 1
 NCCL_UNIQUE_ID_BYTES = 128
 
+# kernel classes of admm_profile (include/admm_lstm.h)
+PROF_CLASSES = ('sweep', 'trial', 'trial_extra', 'atr_x', 'atr_h', 'qgemm_x', 'qgemm_h', 'resid', 'small',
+                'zgemm', 'comm')
+
 
 class NativeUnavailable(RuntimeError):
     """libadmmlstm.so could not be loaded (not built, or not an MI355X environment)."""
@@ -69,6 +73,8 @@ _SIGNATURES = {
     'admm_comm_unique_id': (c_int, [c_void_p, c_int64]),
     'admm_set_comm': (c_int, [c_void_p, c_void_p, c_int64, c_int, c_int]),
     'admm_get_stats': (c_int, [c_void_p, POINTER(AdmmStats)]),
+    'admm_profile': (c_int, [c_void_p, ctypes.c_uint32]),
+    'admm_profile_read': (c_int, [c_void_p, POINTER(c_double), POINTER(c_int32)]),
     'admm_forward': (c_int, [c_void_p, c_int64, c_int32, c_int32, c_int32, c_int32, c_void_p * 4, c_void_p * 4,
                              c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
 }

@@ -10,6 +10,8 @@
 #include <cstdio>
 #include <cstring>
 #include <string>
+#include <utility>
+#include <vector>
 
 #include "admm_kernels.hpp"
 #include "admm_lstm.h"
@@ -76,9 +78,46 @@ struct AdmmCtx {
   // multi-GPU
   ncclComm_t comm = nullptr;
   int rank = 0, world = 1;
+  // optional live kernel timing (admm_profile): hipEvent pairs around launches of the
+  // selected kernel classes, on the launch stream
+  uint32_t prof_mask = 0;
+  std::vector<hipEvent_t> ev_pool;
+  std::vector<std::pair<int, std::pair<hipEvent_t, hipEvent_t>>> ev_used;
 };
 
 namespace {
+
+hipEvent_t take_event(AdmmCtx* c) {
+  if (!c->ev_pool.empty()) {
+    hipEvent_t e = c->ev_pool.back();
+    c->ev_pool.pop_back();
+    return e;
+  }
+  hipEvent_t e = nullptr;
+  (void)hipEventCreate(&e);
+  return e;
+}
+
+// Records an event pair around the launches issued in its scope when the class is enabled.
+struct ProfScope {
+  AdmmCtx* c;
+  int cls;
+  hipStream_t s;
+  hipEvent_t a = nullptr, b = nullptr;
+  ProfScope(AdmmCtx* c_, int cls_, hipStream_t s_) : c(c_), cls(cls_), s(s_) {
+    if (c->prof_mask & (1u << cls)) {
+      a = take_event(c);
+      b = take_event(c);
+      (void)hipEventRecord(a, s);
+    }
+  }
+  ~ProfScope() {
+    if (a) {
+      (void)hipEventRecord(b, s);
+      c->ev_used.push_back({cls, {a, b}});
+    }
+  }
+};
 
 Weights weights_of(const AdmmCtx* c) {
   Weights w;
@@ -96,13 +135,15 @@ Planes6 planes(float* const p[6]) {
 }
 
 int allreduce_f32(AdmmCtx* c, float* p, size_t n, hipStream_t s) {
-  if (c->world <= 1) return ADMM_OK;
+  if (!c->comm) return ADMM_OK;
+  ProfScope ps(c, ADMM_PROF_COMM, s);
   NCCL_TRY(ncclAllReduce(p, p, n, ncclFloat32, ncclSum, c->comm, s));
   return ADMM_OK;
 }
 
 int allreduce_f64(AdmmCtx* c, double* p, size_t n, hipStream_t s) {
-  if (c->world <= 1) return ADMM_OK;
+  if (!c->comm) return ADMM_OK;
+  ProfScope ps(c, ADMM_PROF_COMM, s);
   NCCL_TRY(ncclAllReduce(p, p, n, ncclFloat64, ncclSum, c->comm, s));
   return ADMM_OK;
 }
@@ -110,6 +151,7 @@ int allreduce_f64(AdmmCtx* c, double* p, size_t n, hipStream_t s) {
 // wy update (admm.py:246-280; admm.no_dual_y.py:226-249)
 int stage_wy(AdmmCtx* c, hipStream_t s) {
   const Geom& g = c->g;
+  ProfScope ps(c, ADMM_PROF_SMALL, s);
   launch_wy_grad(g, c->hp, c->buf.gates[ADMM_H], c->buf.a, c->buf.dual_y, c->buf.wy, c->U, c->wy_slab,
                  c->wy_nsplit, s);
   launch_wy_reduce(g, c->wy_slab, c->wy_nsplit, c->Gy, s);
@@ -136,13 +178,22 @@ int stage_weights(AdmmCtx* c, int side, hipStream_t s) {
   ra.dW = c->dW;
   ra.fw_part = c->fw_part;
   ra.nblk = c->nblk_resid;
-  launch_resid(g, c->hp, ra, s);
+  {
+    ProfScope ps(c, ADMM_PROF_RESID, s);
+    launch_resid(g, c->hp, ra, s);
+  }
   const int ns = atr_splits(g, side);
-  launch_atr(g, side, c->buf.x, c->buf.gates[ADMM_H], c->R, c->gslab, ns, s);
+  {
+    ProfScope ps(c, side == 0 ? ADMM_PROF_ATR_X : ADMM_PROF_ATR_H, s);
+    launch_atr(g, side, c->buf.x, c->buf.gates[ADMM_H], c->R, c->gslab, ns, s);
+  }
   launch_reduce_g(g, side, c->hp, c->gslab, ns, c->G, s);
   int rc = allreduce_f32(c, c->G, (size_t)4 * Kd * g.H, s);
   if (rc) return rc;
-  launch_qgemm(g, side, c->buf.x, c->buf.gates[ADMM_H], c->G, c->Q, s);
+  {
+    ProfScope ps(c, side == 0 ? ADMM_PROF_QGEMM_X : ADMM_PROF_QGEMM_H, s);
+    launch_qgemm(g, side, c->buf.x, c->buf.gates[ADMM_H], c->G, c->Q, s);
+  }
   SelectArgs sa{};
   sa.side = side;
   sa.last_pass = kMaxPasses - 1;
@@ -153,7 +204,10 @@ int stage_weights(AdmmCtx* c, int side, hipStream_t s) {
   sa.found = c->found;
   sa.stats = c->stats;
   for (int pass = 0; pass < kMaxPasses; ++pass) {
-    launch_trial(g, pass, c->zc, c->tgt, c->Q, c->found, c->tr_part, c->nblk_trial, s);
+    {
+      ProfScope ps(c, pass == 0 ? ADMM_PROF_TRIAL : ADMM_PROF_TRIAL_EXTRA, s);
+      launch_trial(g, pass, c->zc, c->tgt, c->Q, c->found, c->tr_part, c->nblk_trial, s);
+    }
     launch_trial_reduce(g, pass, c->tr_part, c->nblk_trial, c->fw_part, c->nblk_resid, c->found, c->tr_sums, s);
     rc = allreduce_f64(c, c->tr_sums, 4 * (kTrialJ + 1), s);
     if (rc) return rc;
@@ -172,7 +226,11 @@ int stage_sweep(AdmmCtx* c, hipStream_t s) {
   sa.S = planes(c->buf.gates);
   sa.L = planes(c->buf.duals);
   sa.zc = c->zc;
-  for (int t = 1; t <= g.T; ++t) launch_sweep_t(g, t, w, c->hp, sa, s);
+  for (int t = 1; t <= g.T; ++t) {
+    ProfScope ps(c, ADMM_PROF_SWEEP, s);
+    launch_sweep_t(g, t, w, c->hp, sa, s);
+  }
+  ProfScope ps(c, ADMM_PROF_SMALL, s);
   launch_ht_partial(g, c->hp, sa.S, sa.L, c->buf.a, c->buf.dual_y, c->buf.wy, c->ht_part, c->ht_nblk, s);
   launch_ht_reduce(c->ht_part, c->ht_nblk, c->ht_sums, s);
   int rc = allreduce_f64(c, c->ht_sums, kHTSums, s);
@@ -270,6 +328,11 @@ int admm_destroy(AdmmCtx* c) {
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   if (c->comm) ncclCommDestroy(c->comm);
+  for (hipEvent_t e : c->ev_pool) (void)hipEventDestroy(e);
+  for (auto& u : c->ev_used) {
+    (void)hipEventDestroy(u.second.first);
+    (void)hipEventDestroy(u.second.second);
+  }
   delete c;
   return ADMM_OK;
 }
@@ -343,7 +406,10 @@ int admm_step(AdmmCtx* c, void* stream) {
   hipStream_t s = (hipStream_t)stream;
   HIP_TRY(hipSetDevice(c->device));
   int rc;
-  if (!c->z_valid) launch_zgemm(c->g, weights_of(c), c->buf.x, c->buf.gates[ADMM_H], c->zc, s);
+  if (!c->z_valid) {
+    ProfScope ps(c, ADMM_PROF_ZGEMM, s);
+    launch_zgemm(c->g, weights_of(c), c->buf.x, c->buf.gates[ADMM_H], c->zc, s);
+  }
   if ((rc = stage_wy(c, s))) return rc;
   if ((rc = stage_weights(c, 0, s))) return rc;
   if ((rc = stage_weights(c, 1, s))) return rc;
@@ -372,10 +438,35 @@ int admm_set_comm(AdmmCtx* c, const void* uid, int64_t id_bytes, int rank, int w
   }
   c->rank = rank;
   c->world = world;
-  if (world == 1) return ADMM_OK;
   ncclUniqueId id;
   std::memcpy(&id, uid, sizeof id);
   NCCL_TRY(ncclCommInitRank(&c->comm, world, id, rank));
+  return ADMM_OK;
+}
+
+int admm_profile(AdmmCtx* c, uint32_t class_mask) {
+  if (!c) return fail(ADMM_EINVAL, "NULL ctx");
+  c->prof_mask = class_mask;
+  return ADMM_OK;
+}
+
+int admm_profile_read(AdmmCtx* c, double* ms, int32_t* count) {
+  if (!c || !ms || !count) return fail(ADMM_EINVAL, "NULL argument");
+  HIP_TRY(hipSetDevice(c->device));
+  for (int i = 0; i < ADMM_PROF_CLASSES; ++i) {
+    ms[i] = 0.0;
+    count[i] = 0;
+  }
+  for (auto& u : c->ev_used) {
+    HIP_TRY(hipEventSynchronize(u.second.second));
+    float t = 0.f;
+    HIP_TRY(hipEventElapsedTime(&t, u.second.first, u.second.second));
+    ms[u.first] += t;
+    count[u.first] += 1;
+    c->ev_pool.push_back(u.second.first);
+    c->ev_pool.push_back(u.second.second);
+  }
+  c->ev_used.clear();
   return ADMM_OK;
 }
 

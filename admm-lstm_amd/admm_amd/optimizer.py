@@ -56,6 +56,7 @@ class AdmmOptimizerBase(object):
         self._device = device
         self._world, self._rank = 1, 0
         self._global_batch = self.batch_size
+        self._distributed = bool(distributed)
         if distributed:
             self._join_process_group()
         self._x = self._device_tensor(self.train_x, 'train_x')
@@ -168,7 +169,7 @@ class AdmmOptimizerBase(object):
                                       ctypes.byref(ctx)), 'admm_create')
         self._ctx = ctx
         self._dual_y_sent = self._dual_y_flag()
-        if self._world > 1:
+        if self._distributed:
             self._connect_comm()
 
     def _join_process_group(self) -> None:
@@ -270,6 +271,20 @@ class AdmmOptimizerBase(object):
             'unresolved': s.unresolved,
             'nonfinite': s.nonfinite,
         }
+
+    def profile(self, classes=()) -> None:
+        """Enable live hipEvent timing of the named kernel classes (``_native.PROF_CLASSES``)."""
+        mask = 0
+        for name in classes:
+            mask |= 1 << N.PROF_CLASSES.index(name)
+        N.check(self._lib.admm_profile(self._ctx, mask), 'admm_profile')
+
+    def profile_read(self) -> dict:
+        """{class: (total_ms, launches)} of the events recorded since the last read (synchronises)."""
+        n = len(N.PROF_CLASSES)
+        ms, cnt = (ctypes.c_double * n)(), (ctypes.c_int32 * n)()
+        N.check(self._lib.admm_profile_read(self._ctx, ms, cnt), 'admm_profile_read')
+        return {name: (ms[i], cnt[i]) for i, name in enumerate(N.PROF_CLASSES) if cnt[i]}
 
     def __del__(self):
         ctx = getattr(self, '_ctx', None)

@@ -1,0 +1,242 @@
+#!/usr/bin/env python
+"""Headline benchmark: ADMM iterations/sec of ``ADMMBasedOptimizer.step()``.
+
+BASELINE.json metric: "ADMM iters/sec at hidden=256, batch=8192, seq=32; 1/2/4/8-GPU
+scaling".  One *step* = one ``step()`` (admm.py:62-78) over the synthetic uniform
+regression problem of SURVEY.md 8(d) (config C3: B=8192, T=32, D=16, H=256, O=1,
+GoogleStock rho/beta), fp32, inputs and state resident in HBM before timing.
+
+Multi-GPU (``torchrun --nproc-per-node N``): one process per GPU, weak scaling --
+every rank owns 8192 samples (C4 at N=8: global batch 65536); the step's batch sums are
+all-reduced with RCCL inside libadmmlstm.so.  ``value`` is the whole-job throughput in
+headline units: batch-8192 ADMM iterations per second = (global_batch / 8192) x it/s
+of the global problem (= it/s at N=1).
+
+Also reported (rank 0):
+* ``roofline`` for the dominant kernel class of the timed region, timed live with
+  hipEvents on the step's stream (admm_profile); algorithmic bytes/flops per launch
+  are those of DESIGN.md "Roofline accounting";
+* ``cpu_baseline``: the CPU oracle (a port of the reference op structure, see
+  oracle/admm_oracle.py) timed on this host on a bounded sample (N=1 only).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, 'admm-lstm_amd'))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+
+PEAK_FP32_MFMA = 157.3e12   # MI355X_MICROARCH.md: Peak FP32 (matrix) 157.3 TFLOPS
+PEAK_HBM = 8.0e12           # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+HEADLINE_B = 8192
+
+CONFIGS = {
+    # name: (B per rank, T, D, H, variant, input generator)
+    'c2': (2048, 16, 16, 64, 'admm', 'uniform'),
+    'c3': (8192, 32, 16, 256, 'admm', 'uniform'),
+    'c5': (4096, 64, 1, 512, 'no_dual_y', 'rw'),
+}
+
+
+def make_data(gen: str, B: int, T: int, D: int, seed_offset: int = 0):
+    """SURVEY.md 8(d) generators (uniform: seed 1234; rw: seed 7)."""
+    if gen == 'uniform':
+        g = torch.Generator().manual_seed(1234 + seed_offset)
+        x = torch.rand(B, T, D, generator=g)
+        y = 0.8 * x.mean((1, 2)).unsqueeze(1) + 0.1 * torch.rand(B, 1, generator=g)
+        return x, y
+    g = torch.Generator().manual_seed(7 + seed_offset)
+    s = torch.cumsum(torch.randn(B + T + 1, generator=g), 0)
+    s = (s - s.min()) / (s.max() - s.min())
+    idx = torch.arange(B).unsqueeze(1) + torch.arange(T).unsqueeze(0)
+    return s[idx].unsqueeze(2).contiguous(), s[torch.arange(B) + T].unsqueeze(1).contiguous()
+
+
+def roofline_terms(cls: str, B: int, T: int, D: int, H: int):
+    """Algorithmic (flops, bytes) of ONE launch of a kernel class."""
+    f4 = 4  # bytes per fp32
+    if cls == 'sweep':            # one time step: [B, D+H] x [D+H, 4H] + fused gate/dual updates
+        return 2.0 * B * (D + H) * 4 * H, f4 * B * (D + 27 * H)
+    n = float(B) * T * H          # elements of one [B*T, H] plane
+    if cls == 'atr_h':            # G_q = Hprev^T R_q, 4 gates
+        return 2.0 * B * T * H * 4 * H, f4 * (B * T * H + 4 * n)
+    if cls == 'atr_x':
+        return 2.0 * B * T * D * 4 * H, f4 * (B * T * D + 4 * n)
+    if cls == 'qgemm_h':          # Q_q = Hprev G_q
+        return 2.0 * B * T * H * 4 * H, f4 * (B * T * H + 4 * n)
+    if cls == 'qgemm_x':
+        return 2.0 * B * T * D * 4 * H, f4 * (B * T * D + 4 * n)
+    if cls in ('trial', 'trial_extra'):  # read z, tgt, Q per element
+        return 0.0, f4 * 3 * 4 * n
+    if cls == 'resid':            # read z, lam, S (or z, tgt, x); write tgt/z, R
+        return 0.0, f4 * 5 * 4 * n
+    return None
+
+
+def cpu_baseline(cfg_name: str, seconds_hint: float = 20.0):
+    """Time the CPU oracle (reference op structure) on a bounded sample of the workload."""
+    from oracle import admm_oracle as O
+    from parameters import example_parameter_dictionary
+    B, T, D, H, variant, gen = CONFIGS[cfg_name]
+    try:
+        cores = len(os.sched_getaffinity(0))
+    except AttributeError:  # pragma: no cover
+        cores = os.cpu_count() or 1
+    threads = max(1, min(cores, 16))
+    torch.set_num_threads(threads)
+    frac = 4 if B >= 4096 else 1
+    Bs = B // frac
+    x, y = make_data(gen, Bs, T, D)
+    torch.manual_seed(0)
+    W = O.init_weights(D, H, 1)
+    st = O.init_state(x, y, W)
+    stp = O.Stepper(O.Hyper.from_dict(example_parameter_dictionary['GoogleStock'], variant))
+    stp.step(st)                      # step 1 is cheap (zero gradients); time step 2
+    t0 = time.time()
+    stp.step(st)
+    dt = time.time() - t0
+    return {
+        'value': round(1.0 / (dt * frac), 6), 'unit': 'it/s', 'cores': threads, 'kind': 'port',
+        'sample': f'oracle/admm_oracle.py (reference op structure, fp32 torch CPU, {threads} threads): '
+                  f'{cfg_name} shapes T={T} D={D} H={H} at B={Bs} (1/{frac} batch), step 2 timed '
+                  f'({dt:.2f} s), scaled x1/{frac} to B={B}',
+    }
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--gpus', type=int, default=1)
+    ap.add_argument('--steps', type=int, default=20)
+    ap.add_argument('--warmup', type=int, default=3)
+    ap.add_argument('--config', default='c3', choices=sorted(CONFIGS))
+    ap.add_argument('--scaling', default='weak', choices=['weak', 'strong'])
+    ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--profile-classes', default='sweep,trial,trial_extra,atr_x,atr_h,qgemm_x,qgemm_h,resid,small')
+    args = ap.parse_args()
+
+    world = int(os.environ.get('WORLD_SIZE', '1'))
+    rank = int(os.environ.get('RANK', '0'))
+    local_rank = int(os.environ.get('LOCAL_RANK', '0'))
+    if world != args.gpus:
+        print(f'warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE', file=sys.stderr)
+    torch.cuda.set_device(local_rank)
+    dev = torch.device('cuda', local_rank)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group('nccl', device_id=dev)
+
+    import admm
+    from blocks.lstm import LSTM
+    from parameters import example_parameter_dictionary
+    if CONFIGS[args.config][4] == 'no_dual_y':
+        import importlib.util
+        spec = importlib.util.spec_from_file_location('admm_no_dual_y',
+                                                      os.path.join(ROOT, 'admm-lstm_amd', 'admm.no_dual_y.py'))
+        mod = importlib.util.module_from_spec(spec)
+        spec.loader.exec_module(mod)
+    else:
+        mod = admm
+
+    B, T, D, H, variant, gen = CONFIGS[args.config]
+    Bg = B * world if args.scaling == 'weak' else B
+    per = Bg // world
+    x_all, y_all = make_data(gen, Bg, T, D)
+    x = x_all[rank * per:(rank + 1) * per].contiguous().to(dev)
+    y = y_all[rank * per:(rank + 1) * per].contiguous().to(dev)
+    del x_all, y_all
+    torch.manual_seed(0)
+    model = LSTM(D, H, 1).to(dev)
+    opt = mod.ADMMBasedOptimizer(model, (x, y), example_parameter_dictionary['GoogleStock'], verbose=False,
+                                 distributed=world > 1)
+
+    def barrier():
+        torch.cuda.synchronize(dev)
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+
+    for _ in range(args.warmup):
+        opt.step()
+    barrier()
+    classes = [c for c in args.profile_classes.split(',') if c]
+    opt.profile(classes)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        opt.step()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    opt.profile(())
+    prof = opt.profile_read()
+    if dist is not None:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    stats = opt.last_step_stats()
+    loss = float(torch.nn.functional.mse_loss(model(x), y))
+    if dist is not None:
+        lt = torch.tensor([loss * per], dtype=torch.float64, device=dev)
+        dist.all_reduce(lt)
+        loss = float(lt.item()) / Bg
+
+    it_s = args.steps / elapsed
+    value = it_s * Bg / HEADLINE_B
+    # roofline of the dominant kernel class
+    roof = None
+    ranked = sorted(((ms, c) for c, (ms, n) in prof.items() if roofline_terms(c, per, T, D, H)), reverse=True)
+    if ranked:
+        ms, cls = ranked[0]
+        n = prof[cls][1]
+        avg_s = ms / n / 1e3
+        flops, nbytes = roofline_terms(cls, per, T, D, H)
+        t_mfma, t_hbm = flops / PEAK_FP32_MFMA, nbytes / PEAK_HBM
+        if t_mfma >= t_hbm:
+            roof = {'bound': 'mfma', 'achieved': flops / avg_s / 1e12, 'peak': PEAK_FP32_MFMA / 1e12,
+                    'unit': 'TFLOP/s'}
+        else:
+            roof = {'bound': 'hbm', 'achieved': nbytes / avg_s / 1e9, 'peak': PEAK_HBM / 1e9, 'unit': 'GB/s'}
+        roof['frac'] = roof['achieved'] / roof['peak']
+        roof['traffic'] = None
+        roof['kernel'] = cls
+        roof['avg_launch_us'] = avg_s * 1e6
+        roof['launches'] = n
+        roof = {k: (round(v, 4) if isinstance(v, float) else v) for k, v in roof.items()}
+    kernel_ms = {c: {'ms_per_step': round(ms / args.steps, 4), 'launches_per_step': n / args.steps}
+                 for c, (ms, n) in sorted(prof.items(), key=lambda kv: -kv[1][0])}
+
+    if rank == 0:
+        cpu = None
+        if world == 1 and not args.no_cpu_baseline:
+            cpu = cpu_baseline(args.config)
+        out = {
+            'metric': 'ADMM iters/sec at hidden=256, batch=8192, seq=32; 1/2/4/8-GPU scaling',
+            'value': round(value, 4), 'unit': 'it/s', 'n_gpus': world, 'steps': args.steps, 'warmup': args.warmup,
+            'ms_per_step': round(elapsed / args.steps * 1e3, 4), 'higher_is_better': True,
+            'scaling': args.scaling, 'vs_baseline': None, 'dtype': 'f32', 'data': 'synthetic',
+            'config': {'workload': f'{args.config.upper()}: ADMMBasedOptimizer.step() ({variant}), '
+                                   f'uniform synthetic regression' if gen == 'uniform' else
+                                   f'{args.config.upper()}: ADMMBasedOptimizer.step() ({variant}), random-walk windows',
+                       'global_batch': Bg, 'batch_per_gpu': per, 'seq_len': T, 'input_size': D, 'hidden': H,
+                       'output_size': 1, 'params': 'GoogleStock', 'parallelism': f'dp{world}',
+                       'global_it_per_s': round(it_s, 4)},
+            'roofline': roof,
+            'cpu_baseline': cpu,
+            'kernels': kernel_ms,
+            'line_search_k': list(stats['k'].values()),
+            'final_train_mse': loss,
+        }
+        print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == '__main__':
+    main()

@@ -133,6 +133,27 @@ int admm_set_comm(AdmmCtx* ctx, const void* unique_id, int64_t id_bytes, int ran
 
 int admm_get_stats(AdmmCtx* ctx, AdmmStats* out);
 
+/* Live kernel timing (used by bench.py's roofline): when a class bit is set, admm_step
+   records a hipEvent pair around every launch of that class on the step's stream.
+   admm_profile_read waits for them, returns total ms and launch counts per class, and
+   resets.  Classes: */
+enum {
+  ADMM_PROF_SWEEP = 0,        /* k_sweep_t, one launch per time step t */
+  ADMM_PROF_TRIAL = 1,        /* first line-search trial pass (x and h stages) */
+  ADMM_PROF_TRIAL_EXTRA = 2,  /* later trial passes (no-ops once every gate is resolved) */
+  ADMM_PROF_ATR_X = 3,        /* G = X^T R (x stage) */
+  ADMM_PROF_ATR_H = 4,        /* G = Hprev^T R (h stage) */
+  ADMM_PROF_QGEMM_X = 5,      /* Q = X G */
+  ADMM_PROF_QGEMM_H = 6,      /* Q = Hprev G */
+  ADMM_PROF_RESID = 7,        /* residual / target pass of each weight stage */
+  ADMM_PROF_SMALL = 8,        /* wy and h_T kernels */
+  ADMM_PROF_ZGEMM = 9,        /* z-cache recompute (only after external modifications) */
+  ADMM_PROF_COMM = 10,        /* RCCL all-reduces */
+  ADMM_PROF_CLASSES = 11
+};
+int admm_profile(AdmmCtx* ctx, uint32_t class_mask);
+int admm_profile_read(AdmmCtx* ctx, double* ms /* [ADMM_PROF_CLASSES] */, int32_t* count /* [ADMM_PROF_CLASSES] */);
+
 /* LSTM.forward / init_gate_variables (blocks/lstm.py:43-46, 65-88) without a context.
    x [B,T,D]; wx/wh/wy as above; out_a [B,O].  If gates_out is non-NULL it holds six
    [B,T+1,H] tensors that receive i,f,g,o,c,h at t >= 1 (their time-0 slices are the

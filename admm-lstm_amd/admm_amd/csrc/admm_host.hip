@@ -491,6 +491,28 @@ int admm_get_stats(AdmmCtx* c, AdmmStats* out) {
   return ADMM_OK;
 }
 
+int admm_debug_trial(const float* z, const float* tgt, const float* q, int64_t n, int32_t tanh_gate, int32_t kbase,
+                     double* out, void* stream) {
+  if (!z || !tgt || !q || !out || n <= 0) return fail(ADMM_EINVAL, "admm_debug_trial: bad arguments");
+  hipStream_t s = (hipStream_t)stream;
+  const int nblk = 64;
+  double* part = nullptr;
+  int rc = dalloc(&part, (size_t)nblk * kTrialJ);
+  if (rc) return rc;
+  launch_trial_debug(n, tanh_gate, kbase, z, tgt, q, part, nblk, s);
+  std::vector<double> h((size_t)nblk * kTrialJ);
+  hipError_t e = hipMemcpyAsync(h.data(), part, h.size() * sizeof(double), hipMemcpyDeviceToHost, s);
+  if (e == hipSuccess) e = hipStreamSynchronize(s);
+  (void)hipFree(part);
+  if (e != hipSuccess) return fail(ADMM_EHIP, "admm_debug_trial: %s", hipGetErrorString(e));
+  for (int k = 0; k < kTrialJ; ++k) {
+    double acc = 0.0;
+    for (int b = 0; b < nblk; ++b) acc += h[(size_t)b * kTrialJ + k];
+    out[k] = acc;
+  }
+  return ADMM_OK;
+}
+
 int admm_forward(const float* x, int64_t batch, int32_t seq_len, int32_t input_size, int32_t hidden_size,
                  int32_t output_size, const float* const wx[4], const float* const wh[4], const float* wy,
                  float* const gates_out[6], float* h_scratch, float* c_scratch, float* z_out, float* out_a,

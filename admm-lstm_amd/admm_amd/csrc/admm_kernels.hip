@@ -343,40 +343,61 @@ __global__ __launch_bounds__(kThreads) void k_qgemm(Geom g, int side, const floa
 
 // Trial pass: for k in [pass*J, pass*J + J) accumulate
 //   f(W + G/2^k) - f(W) = 0.5 rho sum_e [ (d0 + D)^2 - d0^2 ],  D = phi(z + Q 2^-k) - phi(z),
-// with D evaluated without cancellation (admm_dev.hpp).  The reference evaluates f(beta)
-// and f(W) separately in fp32 and compares them (admm.py:327-334); see DESIGN.md.
+// with D evaluated without cancellation (admm_dev.hpp, trial_delta).  The reference
+// evaluates f(beta) and f(W) separately in fp32 and compares them (admm.py:327-334); see
+// DESIGN.md.  Elements are streamed as float4 when H % 4 == 0.
+template <bool TANH>
+__device__ __forceinline__ void trial_accumulate(float z, float tg, float qv, float scale0, float (&acc)[kTrialJ]) {
+  const TrialElem e = TANH ? trial_elem_tanh(z, tg) : trial_elem_sigmoid(z, tg);
+  float sc = scale0;
+#pragma unroll
+  for (int k = 0; k < kTrialJ; ++k) {
+    const float D = trial_delta<TANH>(e, qv * sc);   // sc = 2^-(kbase+k): exact scaling
+    acc[k] += D * (2.f * e.d0 + D);
+    sc *= 0.5f;
+  }
+}
+
+template <bool TANH, int VEC>
+__device__ __forceinline__ void trial_loop(int64_t n, const float* zq, const float* tq, const float* Qq, float scale0,
+                                           float (&acc)[kTrialJ]) {
+  const int64_t nv = n / VEC;
+  const int64_t stride = (int64_t)gridDim.x * kThreads;
+  for (int64_t v = (int64_t)blockIdx.x * kThreads + threadIdx.x; v < nv; v += stride) {
+    if (VEC == 4) {
+      const float4 z4 = reinterpret_cast<const float4*>(zq)[v];
+      const float4 t4 = reinterpret_cast<const float4*>(tq)[v];
+      const float4 q4 = reinterpret_cast<const float4*>(Qq)[v];
+      trial_accumulate<TANH>(z4.x, t4.x, q4.x, scale0, acc);
+      trial_accumulate<TANH>(z4.y, t4.y, q4.y, scale0, acc);
+      trial_accumulate<TANH>(z4.z, t4.z, q4.z, scale0, acc);
+      trial_accumulate<TANH>(z4.w, t4.w, q4.w, scale0, acc);
+    } else {
+      trial_accumulate<TANH>(zq[v], tq[v], Qq[v], scale0, acc);
+    }
+  }
+}
+
 __global__ __launch_bounds__(kThreads) void k_trial(Geom g, int pass, const float* zc, const float* tgt,
                                                       const float* Q, const int* found, double* part, int nblk) {
   __shared__ double red[4][kTrialJ];
   const int q = blockIdx.y;
   if (found[q]) return;
-  const bool th = (q == 2);
-  const int64_t BT = g.BT(), n = BT * g.H;
+  const int64_t n = g.BT() * g.H;
   const float* zq = zc + (int64_t)q * n;
   const float* tq = tgt + (int64_t)q * n;
   const float* Qq = Q + (int64_t)q * n;
   float acc[kTrialJ];
 #pragma unroll
   for (int k = 0; k < kTrialJ; ++k) acc[k] = 0.f;
-  const int kbase = pass * kTrialJ;
-  for (int64_t e = (int64_t)blockIdx.x * kThreads + threadIdx.x; e < n; e += (int64_t)gridDim.x * kThreads) {
-    const float z = zq[e], tg = tq[e], qv = Qq[e];
-    if (th) {
-      const float u = tanhf(z), sz = sech(z), d0 = u - tg;
-#pragma unroll
-      for (int k = 0; k < kTrialJ; ++k) {
-        const float D = dtanh(z, ldexpf(qv, -(kbase + k)), u, sz);
-        acc[k] += D * (2.f * d0 + D);
-      }
-    } else {
-      const SigPair sp = sig_pair(z);
-      const float d0 = sp.s - tg;
-#pragma unroll
-      for (int k = 0; k < kTrialJ; ++k) {
-        const float D = dsigmoid(z, ldexpf(qv, -(kbase + k)), sp.s, sp.sc);
-        acc[k] += D * (2.f * d0 + D);
-      }
-    }
+  const float scale0 = ldexpf(1.f, -pass * kTrialJ);
+  const bool vec = (g.H % 4) == 0;
+  if (q == 2) {
+    if (vec) trial_loop<true, 4>(n, zq, tq, Qq, scale0, acc);
+    else trial_loop<true, 1>(n, zq, tq, Qq, scale0, acc);
+  } else {
+    if (vec) trial_loop<false, 4>(n, zq, tq, Qq, scale0, acc);
+    else trial_loop<false, 1>(n, zq, tq, Qq, scale0, acc);
   }
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
 #pragma unroll
@@ -388,6 +409,29 @@ __global__ __launch_bounds__(kThreads) void k_trial(Geom g, int pass, const floa
   if (threadIdx.x < kTrialJ) {
     const int k = threadIdx.x;
     part[((int64_t)q * kTrialJ + k) * nblk + blockIdx.x] = (red[0][k] + red[1][k]) + (red[2][k] + red[3][k]);
+  }
+}
+
+// Test hook: the same per-element arithmetic on caller data (one gate), partial sums per block.
+__global__ __launch_bounds__(kThreads) void k_trial_debug(int64_t n, int tanh_gate, int kbase, const float* z,
+                                                            const float* tgt, const float* qv, double* part) {
+  __shared__ double red[4][kTrialJ];
+  float acc[kTrialJ];
+#pragma unroll
+  for (int k = 0; k < kTrialJ; ++k) acc[k] = 0.f;
+  const float scale0 = ldexpf(1.f, -kbase);
+  if (tanh_gate) trial_loop<true, 1>(n, z, tgt, qv, scale0, acc);
+  else trial_loop<false, 1>(n, z, tgt, qv, scale0, acc);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+  for (int k = 0; k < kTrialJ; ++k) {
+    const float s = wave_sum(acc[k]);
+    if (lane == 0) red[w][k] = (double)s;
+  }
+  __syncthreads();
+  if (threadIdx.x < kTrialJ) {
+    const int k = threadIdx.x;
+    part[(int64_t)blockIdx.x * kTrialJ + k] = (red[0][k] + red[1][k]) + (red[2][k] + red[3][k]);
   }
 }
 
@@ -772,6 +816,11 @@ void launch_trial(const Geom& g, int pass, const float* zc, const float* tgt, co
                   double* part, int nblk, hipStream_t s) {
   dim3 grid(nblk, 4);
   k_trial<<<grid, kThreads, 0, s>>>(g, pass, zc, tgt, Q, found, part, nblk);
+}
+
+void launch_trial_debug(int64_t n, int tanh_gate, int kbase, const float* z, const float* tgt, const float* q,
+                        double* part, int nblk, hipStream_t s) {
+  k_trial_debug<<<nblk, kThreads, 0, s>>>(n, tanh_gate, kbase, z, tgt, q, part);
 }
 
 void launch_trial_reduce(const Geom& g, int pass, const double* part, int nblk, const double* fw_part, int fw_nblk,

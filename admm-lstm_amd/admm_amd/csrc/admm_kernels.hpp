@@ -101,6 +101,9 @@ void launch_qgemm(const Geom& g, int side, const float* x, const float* Sh, cons
 int trial_blocks(const Geom& g);
 void launch_trial(const Geom& g, int pass, const float* zc, const float* tgt, const float* Q, const int* found,
                   double* part, int nblk, hipStream_t s);
+// test hook: part[blk][J] for caller-provided z, tgt, q of one gate
+void launch_trial_debug(int64_t n, int tanh_gate, int kbase, const float* z, const float* tgt, const float* q,
+                        double* part, int nblk, hipStream_t s);
 // sums[q][0..J) = sum_blk part ; sums[q][J] = f(W) partial sum
 void launch_trial_reduce(const Geom& g, int pass, const double* part, int nblk, const double* fw_part,
                          int fw_nblk, const int* found, double* sums, hipStream_t s);

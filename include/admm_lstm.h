@@ -154,6 +154,12 @@ enum {
 int admm_profile(AdmmCtx* ctx, uint32_t class_mask);
 int admm_profile_read(AdmmCtx* ctx, double* ms /* [ADMM_PROF_CLASSES] */, int32_t* count /* [ADMM_PROF_CLASSES] */);
 
+/* Test hook (synchronous): the line-search trial arithmetic of one gate on caller data.
+   out[k] (host, 16 doubles) = sum_e [(phi(z_e + q_e 2^-(kbase+k)) - tgt_e)^2 - (phi(z_e) - tgt_e)^2],
+   phi = tanh if tanh_gate else sigmoid (the increment form of admm.py:316-334). */
+int admm_debug_trial(const float* z, const float* tgt, const float* q, int64_t n, int32_t tanh_gate, int32_t kbase,
+                     double* out, void* stream);
+
 /* LSTM.forward / init_gate_variables (blocks/lstm.py:43-46, 65-88) without a context.
    x [B,T,D]; wx/wh/wy as above; out_a [B,O].  If gates_out is non-NULL it holds six
    [B,T+1,H] tensors that receive i,f,g,o,c,h at t >= 1 (their time-0 slices are the

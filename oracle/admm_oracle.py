@@ -169,9 +169,10 @@ def _dact(q: str):
 class Stepper:
     """Runs ``step()`` on a ``State`` (admm.py:62-78 / admm.no_dual_y.py:52-66)."""
 
-    def __init__(self, hyper: Hyper, comm=None):
+    def __init__(self, hyper: Hyper, comm=None, trace_fw: bool = False):
         self.hp = hyper
         self.comm = comm or _LocalComm()
+        self.trace_fw = trace_fw  # also record f(W) per search (one extra objective pass; off when timing)
 
     # -- accessors that copy, like the reference's getters (admm.py:187-222)
     def _slice(self, store, q, t):
@@ -279,7 +280,10 @@ class Stepper:
         theta /= 2
         bq = self.hp.beta[name].clone().detach()
         st.W[name] = (0.5 * rq * T * theta * w - grad) / (bq + 0.5 * rq * theta * T)
-        return {'name': name, 'k': len(tests) - 1, 'tests': tests}
+        rec = {'name': name, 'k': len(tests) - 1, 'tests': tests}
+        if self.trace_fw:
+            rec['f_w'] = float(f(w))
+        return rec
 
     # -- i, f, g, o closed forms (admm.py:353-386)
     def _gate(self, st: State, q: str, t: int):

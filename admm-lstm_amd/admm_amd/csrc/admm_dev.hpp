@@ -135,64 +135,139 @@ __device__ __forceinline__ T block_sum(T v, T* red /* >= 4 entries of LDS */) {
 
 // ----------------------------------------------------------------------------- MFMA tile engine
 //
-// C[BM x BN] += A[BM x K] * B[K x BN], K streamed in chunks of KC through LDS.
-// Waves are laid out (BM/WM) x (BN/WN) (must be 4); each wave owns (WM/32) x (WN/32)
-// 32x32 accumulators.  Fragment maps of v_mfma_f32_32x32x2_f32 (gfx950):
-//   A: lane l holds A[i = l&31][k = l>>5];  B: B[k = l>>5][j = l&31];
-//   C/D register r: row = (r&3) + 8*(r>>2) + 4*(l>>5), col = l&31.
-// The operand source P provides a(m, k) and b(k, n) global loads (returning 0 outside the
-// problem) and A_M_FAST (which index is contiguous in memory, for coalesced staging).
+// C[BM x BN] += A[BM x K] * B[K x BN] over K in chunks of KC, fp32 in / fp32 accumulate
+// (v_mfma_f32_32x32x2_f32: exact f32 products, k-ordered fma chain).
+// Fragment maps (gfx950): A: lane l holds A[i = l&31][k = l>>5]; B: B[k = l>>5][j = l&31];
+// C/D register r: row = (r&3) + 8*(r>>2) + 4*(l>>5), col = l&31.
+//
+// LDS images are k-major, As[k][m] and Bs[k][n], so every fragment read is a
+// ds_read_b32 of 32 consecutive dwords per half-wave (conflict-free).  Global -> LDS
+// staging is float4 and software-pipelined through registers: the loads of chunk c+1
+// are issued before the MFMAs of chunk c and written to LDS after them.
+//
+// Operand source P supplies, per chunk, float4 loads of A and B:
+//   P::A_ROW_MAJOR  true : A is [m][k] in memory -> float4 = 4 consecutive k of row m
+//                   false: A is [k][m] in memory -> float4 = 4 consecutive m of row k
+//   a4(m, k), b4(k, n): float4 at (m, k) / (k, n); zero outside the problem.
+//   B is always [k][n] -> float4 = 4 consecutive n.
 
-template <int BM, int BN, int WM, int WN>
-struct TileShape {
-  static constexpr int KC = 16;
+template <int BM, int BN, int WM, int WN, int KC>
+struct Tile {
   static constexpr int MT = WM / 32, NT = WN / 32;
   static constexpr int WAVES_N = BN / WN;
   static_assert((BM / WM) * (BN / WN) == 4, "4 waves per workgroup");
-  static constexpr int A_STRIDE = KC + 1;  // +1 dword: conflict-free ds_read_b32 down a column
-  static constexpr int LDS_FLOATS = BM * A_STRIDE + KC * BN;
+  static_assert(KC % 4 == 0 && BM % 4 == 0 && BN % 4 == 0, "float4 staging");
+  static constexpr int AS = BM + 4, BS = BN + 4;     // LDS row strides (dwords)
+  static constexpr int STAGE_FLOATS = KC * AS + KC * BS;
+  static constexpr int LDS_FLOATS = 2 * STAGE_FLOATS;  // double-buffered
+  static constexpr int A4 = BM * KC / 4, B4 = BN * KC / 4;
+  static constexpr int A_PER = (A4 + kThreads - 1) / kThreads, B_PER = (B4 + kThreads - 1) / kThreads;
 };
+
+// XCD-aware block order (cdna_hip_programming.md T1): blocks are dealt round-robin over the
+// 8 XCDs, so hand each XCD a contiguous range of logical tiles -- tiles that share operand
+// rows then run on one L2.  Bijective for any grid size.
+__device__ __forceinline__ int xcd_swizzle(int bid, int nb) {
+  constexpr int NX = 8;
+  const int q = nb / NX, r = nb % NX;
+  const int x = bid % NX, i = bid / NX;
+  // XCD x owns q (+1 if x < r) consecutive logical ids
+  return x * q + (x < r ? x : r) + i;
+}
 
 __device__ __forceinline__ int acc_row(int r, int lane) { return (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5); }
 
-template <int BM, int BN, int WM, int WN, class P>
-__device__ __forceinline__ void gemm_tile(const P& p, int64_t m0, int64_t n0, int64_t k0, int64_t k1,
-                                          f32x16 (&acc)[WM / 32][WN / 32], float* smem) {
-  using S = TileShape<BM, BN, WM, WN>;
-  constexpr int KC = S::KC;
-  float* As = smem;
-  float* Bs = smem + BM * S::A_STRIDE;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm0 = (wave / S::WAVES_N) * WM, wn0 = (wave % S::WAVES_N) * WN;
+template <int BM, int BN, int WM, int WN, int KC, class P>
+struct Engine {
+  using S = Tile<BM, BN, WM, WN, KC>;
+  float4 ra[S::A_PER], rb[S::B_PER];
 
-  for (int64_t kb = k0; kb < k1; kb += KC) {
-    const int kn = (int)((k1 - kb) < KC ? (k1 - kb) : KC);
-    for (int i = tid; i < BM * KC; i += kThreads) {
-      int m, k;
-      if (P::A_M_FAST) { m = i % BM; k = i / BM; } else { k = i % KC; m = i / KC; }
-      As[m * S::A_STRIDE + k] = (k < kn) ? p.a(m0 + m, kb + k) : 0.f;
+  __device__ __forceinline__ void load(const P& p, int64_t m0, int64_t n0, int64_t kb) {
+    const int tid = threadIdx.x;
+#pragma unroll
+    for (int i = 0; i < S::A_PER; ++i) {
+      const int f = tid + i * kThreads;
+      if (f < S::A4) {
+        if (P::A_ROW_MAJOR) ra[i] = p.a4(m0 + f / (KC / 4), kb + 4 * (f % (KC / 4)));
+        else ra[i] = p.a4(m0 + 4 * (f % (BM / 4)), kb + f / (BM / 4));
+      }
     }
-    for (int i = tid; i < KC * BN; i += kThreads) {
-      const int n = i % BN, k = i / BN;
-      Bs[k * BN + n] = (k < kn) ? p.b(kb + k, n0 + n) : 0.f;
+#pragma unroll
+    for (int i = 0; i < S::B_PER; ++i) {
+      const int f = tid + i * kThreads;
+      if (f < S::B4) rb[i] = p.b4(kb + f / (BN / 4), n0 + 4 * (f % (BN / 4)));
     }
-    __syncthreads();
+  }
+
+  __device__ __forceinline__ void store(float* As, float* Bs) const {
+    const int tid = threadIdx.x;
+#pragma unroll
+    for (int i = 0; i < S::A_PER; ++i) {
+      const int f = tid + i * kThreads;
+      if (f < S::A4) {
+        if (P::A_ROW_MAJOR) {
+          const int m = f / (KC / 4), k = 4 * (f % (KC / 4));
+          As[(k + 0) * S::AS + m] = ra[i].x;
+          As[(k + 1) * S::AS + m] = ra[i].y;
+          As[(k + 2) * S::AS + m] = ra[i].z;
+          As[(k + 3) * S::AS + m] = ra[i].w;
+        } else {
+          const int m = 4 * (f % (BM / 4)), k = f / (BM / 4);
+          *reinterpret_cast<float4*>(&As[k * S::AS + m]) = ra[i];
+        }
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < S::B_PER; ++i) {
+      const int f = tid + i * kThreads;
+      if (f < S::B4) *reinterpret_cast<float4*>(&Bs[(f / (BN / 4)) * S::BS + 4 * (f % (BN / 4))]) = rb[i];
+    }
+  }
+
+  __device__ __forceinline__ static void compute(const float* As, const float* Bs,
+                                                 f32x16 (&acc)[S::MT][S::NT]) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int wm0 = (wave / S::WAVES_N) * WM, wn0 = (wave % S::WAVES_N) * WN;
+    const int kh = lane >> 5, c = lane & 31;
 #pragma unroll
     for (int kk = 0; kk < KC; kk += 2) {
       float av[S::MT], bv[S::NT];
 #pragma unroll
-      for (int mi = 0; mi < S::MT; ++mi) av[mi] = As[(wm0 + mi * 32 + (lane & 31)) * S::A_STRIDE + kk + (lane >> 5)];
+      for (int mi = 0; mi < S::MT; ++mi) av[mi] = As[(kk + kh) * S::AS + wm0 + mi * 32 + c];
 #pragma unroll
-      for (int ni = 0; ni < S::NT; ++ni) bv[ni] = Bs[(kk + (lane >> 5)) * BN + wn0 + ni * 32 + (lane & 31)];
+      for (int ni = 0; ni < S::NT; ++ni) bv[ni] = Bs[(kk + kh) * S::BS + wn0 + ni * 32 + c];
 #pragma unroll
       for (int mi = 0; mi < S::MT; ++mi)
 #pragma unroll
         for (int ni = 0; ni < S::NT; ++ni)
           acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[mi], bv[ni], acc[mi][ni], 0, 0, 0);
     }
-    __syncthreads();
   }
-}
+
+  // Whole K loop: [k0, k1) in chunks of KC.  Two LDS stages: while the MFMAs consume
+  // stage c%2, the global loads of chunk c+1 are in flight and then written to the other
+  // stage; one barrier per chunk (the stage written at chunk c was last read at c-1).
+  __device__ __forceinline__ void run(const P& p, int64_t m0, int64_t n0, int64_t k0, int64_t k1,
+                                      f32x16 (&acc)[S::MT][S::NT], float* smem) {
+    if (k0 >= k1) return;
+    load(p, m0, n0, k0);
+    store(smem, smem + KC * S::AS);
+    __syncthreads();
+    int stage = 0;
+    for (int64_t kb = k0; kb < k1; kb += KC) {
+      const bool more = kb + KC < k1;
+      if (more) load(p, m0, n0, kb + KC);
+      float* cur = smem + stage * S::STAGE_FLOATS;
+      compute(cur, cur + KC * S::AS, acc);
+      if (more) {
+        float* nxt = smem + (stage ^ 1) * S::STAGE_FLOATS;
+        store(nxt, nxt + KC * S::AS);
+      }
+      __syncthreads();
+      stage ^= 1;
+    }
+  }
+};
 
 template <int MT, int NT>
 __device__ __forceinline__ void zero_acc(f32x16 (&acc)[MT][NT]) {

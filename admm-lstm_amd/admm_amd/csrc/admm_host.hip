@@ -9,6 +9,7 @@
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
+#include <algorithm>
 #include <string>
 #include <utility>
 #include <vector>
@@ -66,9 +67,8 @@ struct AdmmCtx {
   // workspace (all device)
   float *zc = nullptr, *tgt = nullptr, *R = nullptr, *Q = nullptr;  // [4][BT][H]
   float *G = nullptr, *dW = nullptr, *gslab = nullptr;
-  int nsplit_max = 1;
-  double *fw_part = nullptr, *tr_part = nullptr, *tr_sums = nullptr;
-  int nblk_resid = 1, nblk_trial = 1;
+  double *tr_part = nullptr, *tr_sums = nullptr, *tr_poly = nullptr;
+  int nblk_resid = 1, nblk_trial = 1, nblk_rx = 1;
   int* found = nullptr;
   float *U = nullptr, *wy_slab = nullptr, *Gy = nullptr;
   int wy_nsplit = 1;
@@ -166,38 +166,52 @@ int stage_wy(AdmmCtx* c, hipStream_t s) {
 int stage_weights(AdmmCtx* c, int side, hipStream_t s) {
   const Geom& g = c->g;
   const int Kd = side == 0 ? g.D : g.H;
+  const bool fast = fast_path(g);
+  const Planes6 S = planes(c->buf.gates), L = planes(c->buf.duals);
   HIP_TRY(hipMemsetAsync(c->found, 0, 4 * sizeof(int), s));
-  ResidArgs ra{};
-  ra.stage = side;
-  ra.x = c->buf.x;
-  ra.S = planes(c->buf.gates);
-  ra.L = planes(c->buf.duals);
-  ra.zc = c->zc;
-  ra.tgt = c->tgt;
-  ra.R = c->R;
-  ra.dW = c->dW;
-  ra.fw_part = c->fw_part;
-  ra.nblk = c->nblk_resid;
-  {
+  int ns;
+  // 1. G_q = rho_q sum_rows A^T R_q
+  if (fast && side == 0) {
+    ns = c->nblk_rx;
     ProfScope ps(c, ADMM_PROF_RESID, s);
-    launch_resid(g, c->hp, ra, s);
-  }
-  const int ns = atr_splits(g, side);
-  {
+    launch_resid_gx(g, c->hp, c->buf.x, S, L, c->zc, c->tgt, c->gslab, ns, s);
+  } else if (fast) {
+    ns = atr_splits(g, 1);
+    ProfScope ps(c, ADMM_PROF_ATR_H, s);
+    launch_atr_fused(g, c->hp, c->buf.x, c->buf.gates[ADMM_H], c->zc, c->tgt, c->dW, c->gslab, ns, s);
+  } else {
+    ResidArgs ra{};
+    ra.stage = side;
+    ra.x = c->buf.x;
+    ra.S = S;
+    ra.L = L;
+    ra.zc = c->zc;
+    ra.tgt = c->tgt;
+    ra.R = c->R;
+    ra.dW = c->dW;
+    ra.nblk = c->nblk_resid;
+    {
+      ProfScope ps(c, ADMM_PROF_RESID, s);
+      launch_resid(g, c->hp, ra, s);
+    }
+    ns = atr_splits(g, side);
     ProfScope ps(c, side == 0 ? ADMM_PROF_ATR_X : ADMM_PROF_ATR_H, s);
     launch_atr(g, side, c->buf.x, c->buf.gates[ADMM_H], c->R, c->gslab, ns, s);
   }
   launch_reduce_g(g, side, c->hp, c->gslab, ns, c->G, s);
   int rc = allreduce_f32(c, c->G, (size_t)4 * Kd * g.H, s);
   if (rc) return rc;
-  {
+  // 2. trial direction Q = A G (not needed on the fast x side: formed inside the trials)
+  if (!(fast && side == 0)) {
     ProfScope ps(c, side == 0 ? ADMM_PROF_QGEMM_X : ADMM_PROF_QGEMM_H, s);
     launch_qgemm(g, side, c->buf.x, c->buf.gates[ADMM_H], c->G, c->Q, s);
   }
+  // 3. line search: trial passes of kTrialJ exponents each until every gate has passed
   SelectArgs sa{};
   sa.side = side;
   sa.last_pass = kMaxPasses - 1;
   sa.sums = c->tr_sums;
+  sa.poly = c->tr_poly;
   sa.G = c->G;
   for (int q = 0; q < 4; ++q) sa.W[q] = side == 0 ? c->buf.wx[q] : c->buf.wh[q];
   sa.dW = side == 0 ? c->dW : nullptr;
@@ -206,10 +220,14 @@ int stage_weights(AdmmCtx* c, int side, hipStream_t s) {
   for (int pass = 0; pass < kMaxPasses; ++pass) {
     {
       ProfScope ps(c, pass == 0 ? ADMM_PROF_TRIAL : ADMM_PROF_TRIAL_EXTRA, s);
-      launch_trial(g, pass, c->zc, c->tgt, c->Q, c->found, c->tr_part, c->nblk_trial, s);
+      if (fast)
+        launch_trial_fast(g, side, pass, c->zc, c->tgt, side == 1 ? c->Q : nullptr, c->buf.x,
+                          side == 0 ? c->G : c->dW, c->found, c->tr_part, c->nblk_trial, s);
+      else
+        launch_trial(g, pass, c->zc, c->tgt, c->Q, c->found, c->tr_part, c->nblk_trial, s);
     }
-    launch_trial_reduce(g, pass, c->tr_part, c->nblk_trial, c->fw_part, c->nblk_resid, c->found, c->tr_sums, s);
-    rc = allreduce_f64(c, c->tr_sums, 4 * (kTrialJ + 1), s);
+    launch_trial_reduce(g, pass, c->tr_part, c->nblk_trial, c->found, c->tr_sums, s);
+    rc = allreduce_f64(c, c->tr_sums, 4 * kTrialSlots, s);
     if (rc) return rc;
     sa.pass = pass;
     launch_select(g, c->hp, sa, s);
@@ -295,16 +313,19 @@ int admm_create(const AdmmDims* dims, const AdmmParams* params, int device, Admm
   const int Kmax = g.D > g.H ? g.D : g.H;
   c->nblk_resid = resid_blocks(g);
   c->nblk_trial = trial_blocks(g);
-  c->nsplit_max = atr_splits(g, 0) > atr_splits(g, 1) ? atr_splits(g, 0) : atr_splits(g, 1);
+  c->nblk_rx = resid_gx_blocks(g);
+  size_t slab = (size_t)atr_splits(g, 0) * 4 * g.D * g.H;
+  slab = std::max(slab, (size_t)atr_splits(g, 1) * 4 * g.H * g.H);
+  slab = std::max(slab, (size_t)c->nblk_rx * 4 * g.D * g.H);
   c->wy_nsplit = wy_splits(g);
   c->ht_nblk = ht_blocks(g);
-  if ((rc = dalloc(&c->zc, 4 * plane)) || (rc = dalloc(&c->tgt, 4 * plane)) || (rc = dalloc(&c->R, 4 * plane)) ||
+  if ((rc = dalloc(&c->zc, 4 * plane)) || (rc = dalloc(&c->tgt, 4 * plane)) || (rc = dalloc(&c->R, fast_path(g) ? 1 : 4 * plane)) ||
       (rc = dalloc(&c->Q, 4 * plane)) || (rc = dalloc(&c->G, (size_t)4 * Kmax * g.H)) ||
       (rc = dalloc(&c->dW, (size_t)4 * g.D * g.H)) ||
-      (rc = dalloc(&c->gslab, (size_t)c->nsplit_max * 4 * Kmax * g.H)) ||
-      (rc = dalloc(&c->fw_part, (size_t)4 * c->nblk_resid)) ||
-      (rc = dalloc(&c->tr_part, (size_t)4 * kTrialJ * c->nblk_trial)) ||
-      (rc = dalloc(&c->tr_sums, (size_t)4 * (kTrialJ + 1))) || (rc = dalloc(&c->found, 4)) ||
+      (rc = dalloc(&c->gslab, slab)) ||
+      (rc = dalloc(&c->tr_part, (size_t)4 * kTrialSlots * c->nblk_trial)) ||
+      (rc = dalloc(&c->tr_sums, (size_t)4 * kTrialSlots)) || (rc = dalloc(&c->tr_poly, (size_t)4 * kPolyN)) ||
+      (rc = dalloc(&c->found, 4)) ||
       (rc = dalloc(&c->U, (size_t)g.B * g.O)) || (rc = dalloc(&c->wy_slab, (size_t)c->wy_nsplit * g.H * g.O)) ||
       (rc = dalloc(&c->Gy, (size_t)g.H * g.O)) || (rc = dalloc(&c->ht_part, (size_t)c->ht_nblk * kHTSums)) ||
       (rc = dalloc(&c->ht_sums, kHTSums)) || (rc = dalloc(&c->stats, 1))) {
@@ -323,7 +344,7 @@ int admm_create(const AdmmDims* dims, const AdmmParams* params, int device, Admm
 int admm_destroy(AdmmCtx* c) {
   if (!c) return ADMM_OK;
   (void)hipSetDevice(c->device);
-  void* ptrs[] = {c->zc, c->tgt, c->R, c->Q, c->G, c->dW, c->gslab, c->fw_part, c->tr_part, c->tr_sums, c->found,
+  void* ptrs[] = {c->zc, c->tgt, c->R, c->Q, c->G, c->dW, c->gslab, c->tr_part, c->tr_sums, c->tr_poly, c->found,
                   c->U, c->wy_slab, c->Gy, c->ht_part, c->ht_sums, c->stats};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);

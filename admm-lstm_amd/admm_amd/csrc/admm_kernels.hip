@@ -20,34 +20,77 @@ inline int cdiv64(int64_t a, int64_t b) { return (int)((a + b - 1) / b); }
 // Tile: 128 rows (samples) x 128 columns = 4 gates x 32 hidden units; each wave owns 32
 // rows x all 4 gates, so gate q's pre-activation of (b, j) sits in the same lane for every
 // q and the element-wise ADMM updates run straight out of the accumulators.
-constexpr int TS_BM = 128, TS_BN = 128, TS_WM = 32, TS_WN = 128;
-using TSShape = TileShape<TS_BM, TS_BN, TS_WM, TS_WN>;
+constexpr int TS_BM = 128, TS_BN = 128, TS_WM = 32, TS_WN = 128, TS_KC = 32;
+using TSTile = Tile<TS_BM, TS_BN, TS_WM, TS_WN, TS_KC>;
 
-struct StepSrc {
-  const float* x; int64_t x_stride;  // x_t rows
-  const float* h; int64_t h_stride;  // h_{t-1} rows
+__device__ __forceinline__ const float* pick4(const float* const (&p)[4], int q) {
+  return q == 0 ? p[0] : (q == 1 ? p[1] : (q == 2 ? p[2] : p[3]));
+}
+
+// B operand of every "z" GEMM: [Wx_q; Wh_q] of the 4 gates, column n = 32*q + (j - j0).
+template <bool VEC>
+__device__ __forceinline__ float4 weights4(const Weights& w, int D, int H, int j0, int64_t k, int64_t n) {
+  const int q = (int)(n >> 5), j = j0 + (int)(n & 31);
+  const int K = D + H;
+  if (VEC) {
+    if (k >= K || j >= H) return make_float4(0.f, 0.f, 0.f, 0.f);
+    const float* base = k < D ? pick4(w.wx, q) + k * H : pick4(w.wh, q) + (k - D) * H;
+    return *reinterpret_cast<const float4*>(base + j);
+  }
+  float v[4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int jj = j + u;
+    v[u] = (k < K && jj < H && (jj - j0) < 32 * (q + 1))
+               ? (k < D ? pick4(w.wx, q)[k * H + jj] : pick4(w.wh, q)[(k - D) * H + jj])
+               : 0.f;
+  }
+  return make_float4(v[0], v[1], v[2], v[3]);
+}
+
+template <bool VEC>
+struct StepSrc {  // A = [x_t | h_{t-1}] rows (row-major, K = D + H)
+  const float* x; int64_t x_stride;
+  const float* h; int64_t h_stride;
   int64_t B; int D, H;
   Weights w; int j0;
-  static constexpr bool A_M_FAST = false;
-  __device__ float a(int64_t m, int64_t k) const {
-    if (m >= B) return 0.f;
-    return k < D ? x[m * x_stride + k] : h[m * h_stride + (k - D)];
+  static constexpr bool A_ROW_MAJOR = true;
+  __device__ float4 a4(int64_t m, int64_t k) const {
+    const int K = D + H;
+    if (VEC) {
+      if (m >= B || k >= K) return make_float4(0.f, 0.f, 0.f, 0.f);
+      const float* src = k < D ? x + m * x_stride + k : h + m * h_stride + (k - D);
+      return *reinterpret_cast<const float4*>(src);
+    }
+    float v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int64_t kk = k + u;
+      v[u] = (m < B && kk < K) ? (kk < D ? x[m * x_stride + kk] : h[m * h_stride + (kk - D)]) : 0.f;
+    }
+    return make_float4(v[0], v[1], v[2], v[3]);
   }
-  __device__ float b(int64_t k, int64_t n) const {
-    const int q = (int)(n >> 5), j = j0 + (int)(n & 31);
-    if (j >= H) return 0.f;
-    return k < D ? w.wx[q][k * H + j] : w.wh[q][(k - D) * H + j];
-  }
+  __device__ float4 b4(int64_t k, int64_t n) const { return weights4<VEC>(w, D, H, j0, k, n); }
 };
 
+template <bool VEC>
+__device__ __forceinline__ void step_gemm(const Geom& g, int t, const Weights& w, const float* hprev, int64_t hstride,
+                                          const float* x, f32x16 (&acc)[1][4], float* smem, int64_t m0, int j0) {
+  StepSrc<VEC> src{x + (int64_t)(t - 1) * g.D, (int64_t)g.T * g.D, hprev, hstride, g.B, g.D, g.H, w, j0};
+  Engine<TS_BM, TS_BN, TS_WM, TS_WN, TS_KC, StepSrc<VEC>> eng;
+  eng.run(src, m0, 0, 0, g.D + g.H, acc, smem);
+}
+
+template <bool VEC>
 __global__ __launch_bounds__(kThreads) void k_forward_t(Geom g, int t, Weights w, ForwardT a) {
-  __shared__ float smem[TSShape::LDS_FLOATS];
-  const int64_t m0 = (int64_t)blockIdx.x * TS_BM;
-  const int j0 = blockIdx.y * 32;
-  StepSrc src{a.x + (int64_t)(t - 1) * g.D, (int64_t)g.T * g.D, a.hprev, a.hprev_stride, g.B, g.D, g.H, w, j0};
+  __shared__ float smem[TSTile::LDS_FLOATS];
+  const int nj = (g.H + 31) / 32;
+  const int lid = xcd_swizzle(blockIdx.x, gridDim.x);
+  const int64_t m0 = (int64_t)(lid / nj) * TS_BM;
+  const int j0 = (lid % nj) * 32;
   f32x16 acc[1][4];
   zero_acc(acc);
-  gemm_tile<TS_BM, TS_BN, TS_WM, TS_WN>(src, m0, 0, 0, g.D + g.H, acc, smem);
+  step_gemm<VEC>(g, t, w, a.hprev, a.hprev_stride, a.x, acc, smem, m0, j0);
   const int lane = threadIdx.x & 63, wm0 = (threadIdx.x >> 6) * TS_WM;
   const int j = j0 + (lane & 31);
   if (j >= g.H) return;
@@ -79,16 +122,17 @@ __global__ __launch_bounds__(kThreads) void k_forward_t(Geom g, int t, Weights w
 // One ADMM time step t (admm.py:72-76): i, f, g, o (admm.py:353-386), c (388-436),
 // h for t < T (455-457), dual ascent for i, f, g, o, c (504-530).  h_T, a and the
 // duals of h at T are finished by the h_T kernels below.
+template <bool VEC>
 __global__ __launch_bounds__(kThreads) void k_sweep_t(Geom g, int t, Weights w, Hyper hp, SweepT a) {
-  __shared__ float smem[TSShape::LDS_FLOATS];
-  const int64_t m0 = (int64_t)blockIdx.x * TS_BM;
-  const int j0 = blockIdx.y * 32;
+  __shared__ float smem[TSTile::LDS_FLOATS];
+  const int nj = (g.H + 31) / 32;
+  const int lid = xcd_swizzle(blockIdx.x, gridDim.x);
+  const int64_t m0 = (int64_t)(lid / nj) * TS_BM;
+  const int j0 = (lid % nj) * 32;
   const int64_t rs = (int64_t)g.TP() * g.H;  // row stride of a [B,T+1,H] plane
-  StepSrc src{a.x + (int64_t)(t - 1) * g.D, (int64_t)g.T * g.D, a.S.p[5] + (int64_t)(t - 1) * g.H, rs,
-              g.B, g.D, g.H, w, j0};
   f32x16 acc[1][4];
   zero_acc(acc);
-  gemm_tile<TS_BM, TS_BN, TS_WM, TS_WN>(src, m0, 0, 0, g.D + g.H, acc, smem);
+  step_gemm<VEC>(g, t, w, a.S.p[5] + (int64_t)(t - 1) * g.H, rs, a.x, acc, smem, m0, j0);
   const int lane = threadIdx.x & 63, wm0 = (threadIdx.x >> 6) * TS_WM;
   const int j = j0 + (lane & 31);
   if (j >= g.H) return;
@@ -150,30 +194,41 @@ __global__ __launch_bounds__(kThreads) void k_rowdot(int64_t B, int H, int O, co
 // Row index of the weight phase: row = b*T + (t-1), t = 1..T (admm.py:304-311).
 // X row = x + row*D;  Hprev row (S[h] at t-1) = Sh + (row + b)*H  since b*(T+1) + t-1 = row + b.
 
-struct AllRowSrc {  // z cache recompute: A = [X | Hprev] (K = D+H), B = [Wx; Wh]
+template <bool VEC>
+struct AllRowSrc {  // z cache recompute: A = [X | Hprev] over all rows (K = D+H), B = [Wx; Wh]
   const float* x; const float* Sh; int64_t BT; int T, D, H; Weights w; int j0;
-  static constexpr bool A_M_FAST = false;
-  __device__ float a(int64_t m, int64_t k) const {
-    if (m >= BT) return 0.f;
-    return k < D ? x[m * D + k] : Sh[(m + m / T) * H + (k - D)];
+  static constexpr bool A_ROW_MAJOR = true;
+  __device__ float4 a4(int64_t m, int64_t k) const {
+    const int K = D + H;
+    if (VEC) {
+      if (m >= BT || k >= K) return make_float4(0.f, 0.f, 0.f, 0.f);
+      const float* src = k < D ? x + m * D + k : Sh + (m + m / T) * H + (k - D);
+      return *reinterpret_cast<const float4*>(src);
+    }
+    float v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int64_t kk = k + u;
+      v[u] = (m < BT && kk < K) ? (kk < D ? x[m * D + kk] : Sh[(m + m / T) * H + (kk - D)]) : 0.f;
+    }
+    return make_float4(v[0], v[1], v[2], v[3]);
   }
-  __device__ float b(int64_t k, int64_t n) const {
-    const int q = (int)(n >> 5), j = j0 + (int)(n & 31);
-    if (j >= H) return 0.f;
-    return k < D ? w.wx[q][k * H + j] : w.wh[q][(k - D) * H + j];
-  }
+  __device__ float4 b4(int64_t k, int64_t n) const { return weights4<VEC>(w, D, H, j0, k, n); }
 };
 
-__global__ __launch_bounds__(kThreads) void k_zgemm(Geom g, Weights w, const float* x, const float* Sh,
-                                                      float* zc) {
-  __shared__ float smem[TSShape::LDS_FLOATS];
-  const int64_t m0 = (int64_t)blockIdx.x * TS_BM;
-  const int j0 = blockIdx.y * 32;
+template <bool VEC>
+__device__ __forceinline__ void zgemm_body(const Geom& g, const Weights& w, const float* x, const float* Sh, float* zc,
+                                           float* smem) {
+  const int nj = (g.H + 31) / 32;
+  const int lid = xcd_swizzle(blockIdx.x, gridDim.x);
+  const int64_t m0 = (int64_t)(lid / nj) * TS_BM;
+  const int j0 = (lid % nj) * 32;
   const int64_t BT = g.BT();
-  AllRowSrc src{x, Sh, BT, g.T, g.D, g.H, w, j0};
+  AllRowSrc<VEC> src{x, Sh, BT, g.T, g.D, g.H, w, j0};
   f32x16 acc[1][4];
   zero_acc(acc);
-  gemm_tile<TS_BM, TS_BN, TS_WM, TS_WN>(src, m0, 0, 0, g.D + g.H, acc, smem);
+  Engine<TS_BM, TS_BN, TS_WM, TS_WN, TS_KC, AllRowSrc<VEC>> eng;
+  eng.run(src, m0, 0, 0, g.D + g.H, acc, smem);
   const int lane = threadIdx.x & 63, wm0 = (threadIdx.x >> 6) * TS_WM;
   const int j = j0 + (lane & 31);
   if (j >= g.H) return;
@@ -184,6 +239,12 @@ __global__ __launch_bounds__(kThreads) void k_zgemm(Geom g, Weights w, const flo
 #pragma unroll
     for (int q = 0; q < 4; ++q) zc[((int64_t)q * BT + row) * g.H + j] = acc[0][q][r];
   }
+}
+
+template <bool VEC>
+__global__ __launch_bounds__(kThreads) void k_zgemm(Geom g, Weights w, const float* x, const float* Sh, float* zc) {
+  __shared__ float smem[TSTile::LDS_FLOATS];
+  zgemm_body<VEC>(g, w, x, Sh, zc, smem);
 }
 
 // Element loop helper over (row, j) of a [BT][H] plane with cheap index math.
@@ -197,10 +258,9 @@ struct RowJ {
   }
 };
 
-// admm.py:302-314 (residual part) for the 4 gates; also tgt = lam/rho + S (reused by the
-// trials) and f(W) partial sums (admm.py:316-325 at beta = W).
+// Generic path (any D, H): admm.py:302-314 residual for the 4 gates, materialised; also
+// tgt = lam/rho + S (reused by the trials) and, on the h side, z += X dWx written back.
 __global__ __launch_bounds__(kThreads) void k_resid(Geom g, Hyper hp, ResidArgs a) {
-  __shared__ double red[4];
   const int q = blockIdx.y;
   const bool th = (q == 2);
   const float rho = hp.rho[q];
@@ -212,7 +272,6 @@ __global__ __launch_bounds__(kThreads) void k_resid(Geom g, Hyper hp, ResidArgs 
   const float* Lq = a.L.p[q];
   const float* dWq = a.dW ? a.dW + (int64_t)q * g.D * g.H : nullptr;
   RowJ ix(g.H);
-  float fw = 0.f;
   if (ix.rr < ix.rpb) {
     for (int64_t row = (int64_t)blockIdx.x * ix.rpb + ix.rr; row < BT; row += (int64_t)gridDim.x * ix.rpb) {
       const int64_t b = row / g.T;
@@ -240,56 +299,182 @@ __global__ __launch_bounds__(kThreads) void k_resid(Geom g, Hyper hp, ResidArgs 
           phi = sp.s;
           dphi = sp.s * sp.sc;
         }
-        const float d = phi - tg;
-        Rq[e] = d * dphi;
-        fw += d * d;
+        Rq[e] = (phi - tg) * dphi;
       }
     }
   }
-  const double tot = block_sum((double)fw, red);
-  if (threadIdx.x == 0) a.fw_part[(int64_t)q * a.nblk + blockIdx.x] = tot;
 }
 
-// G_q = A^T R_q split over rows: 64 (weight rows) x 128 (hidden units) tiles per gate.
-constexpr int AT_BM = 64, AT_BN = 128, AT_WM = 32, AT_WN = 64;
-using ATShape = TileShape<AT_BM, AT_BN, AT_WM, AT_WN>;
-
-struct AtRSrc {
-  const float* x; const float* Sh; const float* Rq; int side; int T, D, H, Kd;
-  static constexpr bool A_M_FAST = true;
-  __device__ float a(int64_t m, int64_t row) const {  // A^T[m][row]
-    if (m >= Kd) return 0.f;
-    return side == 0 ? x[row * D + m] : Sh[(row + row / T) * H + m];
+// G_q = A^T R_q split over rows.  Side 1 (A = Hprev, Kd = H): 128 x 128 tiles, 2x2 waves
+// of 64x64; side 0 (A = X, Kd = D small): 32 x 128 tiles.
+template <bool VEC>
+struct AtRSrc {  // A^T: A stored [row][m] (m contiguous); B = R[q] [row][j]
+  const float* x; const float* Sh; const float* Rq; int side; int T, D, H, Kd; int64_t rend;
+  static constexpr bool A_ROW_MAJOR = false;
+  __device__ float4 a4(int64_t m, int64_t row) const {
+    if (row >= rend) return make_float4(0.f, 0.f, 0.f, 0.f);
+    const float* base = side == 0 ? x + row * D : Sh + (row + row / T) * H;
+    if (VEC) {
+      if (m >= Kd) return make_float4(0.f, 0.f, 0.f, 0.f);
+      return *reinterpret_cast<const float4*>(base + m);
+    }
+    float v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) v[u] = (m + u < Kd) ? base[m + u] : 0.f;
+    return make_float4(v[0], v[1], v[2], v[3]);
   }
-  __device__ float b(int64_t row, int64_t j) const { return j < H ? Rq[row * H + j] : 0.f; }
+  __device__ float4 b4(int64_t row, int64_t j) const {
+    if (row >= rend) return make_float4(0.f, 0.f, 0.f, 0.f);
+    if (VEC) {
+      if (j >= H) return make_float4(0.f, 0.f, 0.f, 0.f);
+      return *reinterpret_cast<const float4*>(Rq + row * H + j);
+    }
+    float v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) v[u] = (j + u < H) ? Rq[row * H + j + u] : 0.f;
+    return make_float4(v[0], v[1], v[2], v[3]);
+  }
 };
 
-__global__ __launch_bounds__(kThreads) void k_atr(Geom g, int side, const float* x, const float* Sh,
-                                                    const float* R, float* slab, int nsplit) {
-  __shared__ float smem[ATShape::LDS_FLOATS];
+template <int BM, int WM, bool VEC>
+__device__ __forceinline__ void atr_body(const Geom& g, int side, const float* x, const float* Sh, const float* R,
+                                         float* slab, int nsplit, float* smem) {
+  constexpr int BN = 128, WN = (BM == 128) ? 64 : 32, KC = 32;
+  using S = Tile<BM, BN, WM, WN, KC>;
   const int Kd = side == 0 ? g.D : g.H;
-  const int q = blockIdx.z / nsplit, sp = blockIdx.z % nsplit;
+  const int nm = (Kd + BM - 1) / BM, nn = (g.H + BN - 1) / BN;
+  int lid = xcd_swizzle(blockIdx.x, gridDim.x);
+  const int mt = lid % nm; lid /= nm;
+  const int nt = lid % nn; lid /= nn;
+  const int q = lid % 4, sp = lid / 4;
   const int64_t BT = g.BT();
-  const int64_t per = (BT + nsplit - 1) / nsplit;
+  const int64_t per = ((BT + nsplit - 1) / nsplit + KC - 1) / KC * KC;
   const int64_t r0 = sp * per, r1 = (r0 + per < BT) ? r0 + per : BT;
-  const int m0 = blockIdx.x * AT_BM, n0 = blockIdx.y * AT_BN;
-  AtRSrc src{x, Sh, R + (int64_t)q * BT * g.H, side, g.T, g.D, g.H, Kd};
-  f32x16 acc[1][2];
+  const int m0 = mt * BM, n0 = nt * BN;
+  AtRSrc<VEC> src{x, Sh, R + (int64_t)q * BT * g.H, side, g.T, g.D, g.H, Kd, r1};
+  f32x16 acc[S::MT][S::NT];
   zero_acc(acc);
-  if (r0 < r1) gemm_tile<AT_BM, AT_BN, AT_WM, AT_WN>(src, m0, n0, r0, r1, acc, smem);
+  Engine<BM, BN, WM, WN, KC, AtRSrc<VEC>> eng;
+  if (r0 < r1) eng.run(src, m0, n0, r0, r1, acc, smem);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int wm0 = (wave / ATShape::WAVES_N) * AT_WM, wn0 = (wave % ATShape::WAVES_N) * AT_WN;
+  const int wm0 = (wave / S::WAVES_N) * WM, wn0 = (wave % S::WAVES_N) * WN;
   float* out = slab + ((int64_t)sp * 4 + q) * Kd * g.H;
 #pragma unroll
-  for (int ni = 0; ni < 2; ++ni) {
-    const int j = n0 + wn0 + ni * 32 + (lane & 31);
-    if (j >= g.H) continue;
+  for (int mi = 0; mi < S::MT; ++mi)
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int m = m0 + wm0 + acc_row(r, lane);
-      if (m < Kd) out[(int64_t)m * g.H + j] = acc[0][ni][r];
+    for (int ni = 0; ni < S::NT; ++ni) {
+      const int j = n0 + wn0 + ni * 32 + (lane & 31);
+      if (j >= g.H) continue;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = m0 + wm0 + mi * 32 + acc_row(r, lane);
+        if (m < Kd) out[(int64_t)m * g.H + j] = acc[mi][ni][r];
+      }
     }
+}
+
+template <int BM, int WM, bool VEC>
+__global__ __launch_bounds__(kThreads) void k_atr(Geom g, int side, const float* x, const float* Sh,
+                                                    const float* R, float* slab, int nsplit) {
+  __shared__ float smem[Tile<BM, 128, WM, (BM == 128) ? 64 : 32, 32>::LDS_FLOATS];
+  atr_body<BM, WM, VEC>(g, side, x, Sh, R, slab, nsplit, smem);
+}
+
+// h-stage A^T R with the residual formed in the B-operand loader (admm.py:302-312, h side):
+// z = zc + x_row . dWx (the x-side update, already applied to the weights), then
+// R = (phi(z) - tgt) phi'(z).  R is never materialised.
+template <bool TANH>
+struct AtRFusedSrc {
+  const float* Sh; const float* zq; const float* tq; const float* x; const float* dWl;  // dWl: LDS [D][128]
+  int T, D, H; int64_t rend; int n0;
+  static constexpr bool A_ROW_MAJOR = false;
+  __device__ float4 a4(int64_t m, int64_t row) const {
+    if (row >= rend || m >= H) return make_float4(0.f, 0.f, 0.f, 0.f);
+    return *reinterpret_cast<const float4*>(Sh + (row + row / T) * H + m);
   }
+  __device__ float4 b4(int64_t row, int64_t j) const {
+    if (row >= rend || j >= H) return make_float4(0.f, 0.f, 0.f, 0.f);
+    const int64_t e = row * H + j;
+    float4 z4 = *reinterpret_cast<const float4*>(zq + e);
+    const float4 t4 = *reinterpret_cast<const float4*>(tq + e);
+    const float* wl = dWl + (j - n0);
+#pragma unroll
+    for (int d = 0; d < kFastD; ++d) {
+      if (d < D) {
+        const float xd = x[row * D + d];
+        const float4 w = *reinterpret_cast<const float4*>(wl + d * 128);
+        z4.x += xd * w.x; z4.y += xd * w.y; z4.z += xd * w.z; z4.w += xd * w.w;
+      }
+    }
+    float zz[4] = {z4.x, z4.y, z4.z, z4.w}, tt[4] = {t4.x, t4.y, t4.z, t4.w}, r[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      float phi, dphi;
+      if (TANH) {
+        phi = tanhf(zz[u]);
+        dphi = 1.f - phi * phi;
+      } else {
+        const SigPair sp = sig_pair(zz[u]);
+        phi = sp.s;
+        dphi = sp.s * sp.sc;
+      }
+      r[u] = (phi - tt[u]) * dphi;
+    }
+    return make_float4(r[0], r[1], r[2], r[3]);
+  }
+};
+
+template <bool TANH>
+__device__ __forceinline__ void atr_fused_body(const Geom& g, const float* x, const float* Sh, const float* zc,
+                                               const float* tgt, const float* dW, float* slab, int nsplit,
+                                               float* smem) {
+  constexpr int BM = 128, BN = 128, WM = 64, WN = 64, KC = 32;
+  using S = Tile<BM, BN, WM, WN, KC>;
+  const int nm = (g.H + BM - 1) / BM, nn = (g.H + BN - 1) / BN;
+  int lid = xcd_swizzle(blockIdx.x, gridDim.x);
+  const int mt = lid % nm; lid /= nm;
+  const int nt = lid % nn; lid /= nn;
+  const int q = lid % 4, sp = lid / 4;
+  const int64_t BT = g.BT(), n = BT * g.H;
+  const int64_t per = ((BT + nsplit - 1) / nsplit + KC - 1) / KC * KC;
+  const int64_t r0 = sp * per, r1 = (r0 + per < BT) ? r0 + per : BT;
+  const int m0 = mt * BM, n0 = nt * BN;
+  float* dWl = smem + S::LDS_FLOATS;   // after both engine stages
+  for (int i = threadIdx.x; i < g.D * BN; i += kThreads) {
+    const int d = i / BN, jj = n0 + i % BN;
+    dWl[i] = jj < g.H ? dW[((int64_t)q * g.D + d) * g.H + jj] : 0.f;
+  }
+  __syncthreads();
+  AtRFusedSrc<TANH> src{Sh, zc + (int64_t)q * n, tgt + (int64_t)q * n, x, dWl, g.T, g.D, g.H, r1, n0};
+  f32x16 acc[S::MT][S::NT];
+  zero_acc(acc);
+  Engine<BM, BN, WM, WN, KC, AtRFusedSrc<TANH>> eng;
+  if (r0 < r1) eng.run(src, m0, n0, r0, r1, acc, smem);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int wm0 = (wave / S::WAVES_N) * WM, wn0 = (wave % S::WAVES_N) * WN;
+  float* out = slab + ((int64_t)sp * 4 + q) * g.H * g.H;
+#pragma unroll
+  for (int mi = 0; mi < S::MT; ++mi)
+#pragma unroll
+    for (int ni = 0; ni < S::NT; ++ni) {
+      const int j = n0 + wn0 + ni * 32 + (lane & 31);
+      if (j >= g.H) continue;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int m = m0 + wm0 + mi * 32 + acc_row(r, lane);
+        if (m < g.H) out[(int64_t)m * g.H + j] = acc[mi][ni][r];
+      }
+    }
+}
+
+constexpr int ATR_FUSED_LDS = Tile<128, 128, 64, 64, 32>::LDS_FLOATS + kFastD * 128;
+
+__global__ __launch_bounds__(kThreads) void k_atr_fused(Geom g, const float* x, const float* Sh, const float* zc,
+                                                          const float* tgt, const float* dW, float* slab, int nsplit) {
+  __shared__ float smem[ATR_FUSED_LDS];
+  const int nm = (g.H + 127) / 128, nn = (g.H + 127) / 128;
+  if ((xcd_swizzle(blockIdx.x, gridDim.x) / (nm * nn)) % 4 == 2) atr_fused_body<true>(g, x, Sh, zc, tgt, dW, slab, nsplit, smem);
+  else atr_fused_body<false>(g, x, Sh, zc, tgt, dW, slab, nsplit, smem);
 }
 
 __global__ __launch_bounds__(kThreads) void k_reduce_g(int Kd, int H, Hyper hp, const float* slab, int nsplit,
@@ -303,32 +488,51 @@ __global__ __launch_bounds__(kThreads) void k_reduce_g(int Kd, int H, Hyper hp, 
   G[i] = (float)s * hp.rho[q];  // (sum_t A_t^T R_t) * rho (admm.py:312)
 }
 
-struct QSrc {
+template <bool VEC>
+struct QSrc {  // A = X or Hprev rows (row-major, K = Kd); B = G_q [Kd][H]
   const float* x; const float* Sh; const float* G; int64_t BT; int side, T, D, H, Kd, j0;
-  static constexpr bool A_M_FAST = false;
-  __device__ float a(int64_t row, int64_t k) const {
-    if (row >= BT || k >= Kd) return 0.f;
-    return side == 0 ? x[row * D + k] : Sh[(row + row / T) * H + k];
+  static constexpr bool A_ROW_MAJOR = true;
+  __device__ float4 a4(int64_t row, int64_t k) const {
+    if (row >= BT) return make_float4(0.f, 0.f, 0.f, 0.f);
+    const float* base = side == 0 ? x + row * D : Sh + (row + row / T) * H;
+    if (VEC) {
+      if (k >= Kd) return make_float4(0.f, 0.f, 0.f, 0.f);
+      return *reinterpret_cast<const float4*>(base + k);
+    }
+    float v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) v[u] = (k + u < Kd) ? base[k + u] : 0.f;
+    return make_float4(v[0], v[1], v[2], v[3]);
   }
-  __device__ float b(int64_t k, int64_t n) const {
+  __device__ float4 b4(int64_t k, int64_t n) const {
     const int q = (int)(n >> 5), j = j0 + (int)(n & 31);
-    if (j >= H || k >= Kd) return 0.f;
-    return G[((int64_t)q * Kd + k) * H + j];
+    if (VEC) {
+      if (k >= Kd || j >= H) return make_float4(0.f, 0.f, 0.f, 0.f);
+      return *reinterpret_cast<const float4*>(G + ((int64_t)q * Kd + k) * H + j);
+    }
+    float v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      v[u] = (k < Kd && j + u < H && (j + u - j0) < 32 * (q + 1)) ? G[((int64_t)q * Kd + k) * H + j + u] : 0.f;
+    return make_float4(v[0], v[1], v[2], v[3]);
   }
 };
 
 // Q_q = A G_q: the trial direction, so that z(W + G/theta) = z(W) + Q / theta exactly.
-__global__ __launch_bounds__(kThreads) void k_qgemm(Geom g, int side, const float* x, const float* Sh,
-                                                      const float* G, float* Q) {
-  __shared__ float smem[TSShape::LDS_FLOATS];
+template <bool VEC>
+__device__ __forceinline__ void qgemm_body(const Geom& g, int side, const float* x, const float* Sh, const float* G,
+                                           float* Q, float* smem) {
   const int Kd = side == 0 ? g.D : g.H;
-  const int64_t m0 = (int64_t)blockIdx.x * TS_BM;
-  const int j0 = blockIdx.y * 32;
+  const int nj = (g.H + 31) / 32;
+  const int lid = xcd_swizzle(blockIdx.x, gridDim.x);
+  const int64_t m0 = (int64_t)(lid / nj) * TS_BM;
+  const int j0 = (lid % nj) * 32;
   const int64_t BT = g.BT();
-  QSrc src{x, Sh, G, BT, side, g.T, g.D, g.H, Kd, j0};
+  QSrc<VEC> src{x, Sh, G, BT, side, g.T, g.D, g.H, Kd, j0};
   f32x16 acc[1][4];
   zero_acc(acc);
-  gemm_tile<TS_BM, TS_BN, TS_WM, TS_WN>(src, m0, 0, 0, Kd, acc, smem);
+  Engine<TS_BM, TS_BN, TS_WM, TS_WN, TS_KC, QSrc<VEC>> eng;
+  eng.run(src, m0, 0, 0, Kd, acc, smem);
   const int lane = threadIdx.x & 63, wm0 = (threadIdx.x >> 6) * TS_WM;
   const int j = j0 + (lane & 31);
   if (j >= g.H) return;
@@ -341,26 +545,88 @@ __global__ __launch_bounds__(kThreads) void k_qgemm(Geom g, int side, const floa
   }
 }
 
-// Trial pass: for k in [pass*J, pass*J + J) accumulate
-//   f(W + G/2^k) - f(W) = 0.5 rho sum_e [ (d0 + D)^2 - d0^2 ],  D = phi(z + Q 2^-k) - phi(z),
-// with D evaluated without cancellation (admm_dev.hpp, trial_delta).  The reference
-// evaluates f(beta) and f(W) separately in fp32 and compares them (admm.py:327-334); see
-// DESIGN.md.  Elements are streamed as float4 when H % 4 == 0.
+template <bool VEC>
+__global__ __launch_bounds__(kThreads) void k_qgemm(Geom g, int side, const float* x, const float* Sh,
+                                                      const float* G, float* Q) {
+  __shared__ float smem[TSTile::LDS_FLOATS];
+  qgemm_body<VEC>(g, side, x, Sh, G, Q, smem);
+}
+
+// Trial pass.  For the line search (admm.py:316-336) each gate needs, for k = 0, 1, ...,
+//   f(W + G/2^k) - f(W) = 0.5 rho sum_e [ (d0 + D_k)^2 - d0^2 ],  D_k = phi(z + q 2^-k) - phi(z),
+// evaluated without cancellation (DESIGN.md "line-search numerics").  Two regimes per element:
+//  * |q| <= 2^-8 (the common case): D_k = a1 s + a2 s^2 + a3 s^3 with s = 2^-k and
+//    a_n = c_n q^n (3-term Taylor, truncation < 1e-8 relative for every k >= 0), so the
+//    increment is a degree-6 polynomial in s whose 6 coefficients are summed once (pass 0)
+//    and cover every exponent;
+//  * otherwise: D_k evaluated per candidate for the pass window k in [pass*J, pass*J + J)
+//    (5-term Taylor for |d| <= 1/16, cancellation-free direct form above).
+// Slot layout per gate: kSlots = [J candidates][6 poly][sum d0^2][#per-candidate elements].
+constexpr int kSlots = kTrialSlots;
+constexpr int kSlotPoly = kTrialJ, kSlotFw = kTrialJ + kPolyN, kSlotNne = kTrialJ + kPolyN + 1;
+
 template <bool TANH>
-__device__ __forceinline__ void trial_accumulate(float z, float tg, float qv, float scale0, float (&acc)[kTrialJ]) {
+__device__ __forceinline__ void trial_accumulate(float z, float tg, float qv, int pass, float (&acc)[kSlots]) {
+  float d0, c1, c2, c3;
+  if (TANH) {
+    const float ez = expf(-2.f * fabsf(z));
+    const float mz = 2.f * ez / (1.f + ez);       // 1 - |tanh z|
+    const float u = copysignf(1.f - mz, z);
+    c1 = mz * (2.f - mz);                         // 1 - u^2
+    c2 = -u * c1;
+    c3 = c1 * (u * u - (1.f / 3.f));
+    d0 = tanhf(z) - tg;                           // the tanh of the stored gate / residual
+  } else {
+    const SigPair sp = sig_pair(z);
+    const float p = sp.s * sp.sc;
+    c1 = p;
+    c2 = 0.5f * p * (sp.sc - sp.s);
+    c3 = p * (1.f - 6.f * p) * (1.f / 6.f);
+    d0 = sp.s - tg;
+  }
+  acc[kSlotFw] += d0 * d0;
+  if (fabsf(qv) <= 0x1p-8f) {
+    if (pass == 0) {
+      const float a1 = c1 * qv, a2 = c2 * qv * qv, a3 = c3 * qv * qv * qv, t = 2.f * d0;
+      acc[kSlotPoly + 0] += t * a1;
+      acc[kSlotPoly + 1] += t * a2 + a1 * a1;
+      acc[kSlotPoly + 2] += t * a3 + 2.f * a1 * a2;
+      acc[kSlotPoly + 3] += a2 * a2 + 2.f * a1 * a3;
+      acc[kSlotPoly + 4] += 2.f * a2 * a3;
+      acc[kSlotPoly + 5] += a3 * a3;
+    }
+    return;
+  }
+  acc[kSlotNne] += 1.f;
   const TrialElem e = TANH ? trial_elem_tanh(z, tg) : trial_elem_sigmoid(z, tg);
-  float sc = scale0;
+  float sc = ldexpf(1.f, -pass * kTrialJ);
 #pragma unroll
   for (int k = 0; k < kTrialJ; ++k) {
-    const float D = trial_delta<TANH>(e, qv * sc);   // sc = 2^-(kbase+k): exact scaling
+    const float D = trial_delta<TANH>(e, qv * sc);   // sc = 2^-(pass*J+k): exact scaling
     acc[k] += D * (2.f * e.d0 + D);
     sc *= 0.5f;
   }
 }
 
+__device__ __forceinline__ void trial_block_store(float (&acc)[kSlots], double* part, int q, int nblk) {
+  __shared__ double red[4][kSlots];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+  for (int k = 0; k < kSlots; ++k) {
+    const float s = wave_sum(acc[k]);
+    if (lane == 0) red[w][k] = (double)s;
+  }
+  __syncthreads();
+  if (threadIdx.x < kSlots) {
+    const int k = threadIdx.x;
+    part[((int64_t)q * kSlots + k) * nblk + blockIdx.x] = (red[0][k] + red[1][k]) + (red[2][k] + red[3][k]);
+  }
+}
+
+// Generic trial pass: materialised z (zc) and Q.
 template <bool TANH, int VEC>
-__device__ __forceinline__ void trial_loop(int64_t n, const float* zq, const float* tq, const float* Qq, float scale0,
-                                           float (&acc)[kTrialJ]) {
+__device__ __forceinline__ void trial_loop(int64_t n, const float* zq, const float* tq, const float* Qq, int pass,
+                                           float (&acc)[kSlots]) {
   const int64_t nv = n / VEC;
   const int64_t stride = (int64_t)gridDim.x * kThreads;
   for (int64_t v = (int64_t)blockIdx.x * kThreads + threadIdx.x; v < nv; v += stride) {
@@ -368,95 +634,244 @@ __device__ __forceinline__ void trial_loop(int64_t n, const float* zq, const flo
       const float4 z4 = reinterpret_cast<const float4*>(zq)[v];
       const float4 t4 = reinterpret_cast<const float4*>(tq)[v];
       const float4 q4 = reinterpret_cast<const float4*>(Qq)[v];
-      trial_accumulate<TANH>(z4.x, t4.x, q4.x, scale0, acc);
-      trial_accumulate<TANH>(z4.y, t4.y, q4.y, scale0, acc);
-      trial_accumulate<TANH>(z4.z, t4.z, q4.z, scale0, acc);
-      trial_accumulate<TANH>(z4.w, t4.w, q4.w, scale0, acc);
+#pragma unroll 1
+      for (int u = 0; u < 4; ++u) {
+        const float zu = u == 0 ? z4.x : (u == 1 ? z4.y : (u == 2 ? z4.z : z4.w));
+        const float tu = u == 0 ? t4.x : (u == 1 ? t4.y : (u == 2 ? t4.z : t4.w));
+        const float qu = u == 0 ? q4.x : (u == 1 ? q4.y : (u == 2 ? q4.z : q4.w));
+        trial_accumulate<TANH>(zu, tu, qu, pass, acc);
+      }
     } else {
-      trial_accumulate<TANH>(zq[v], tq[v], Qq[v], scale0, acc);
+      trial_accumulate<TANH>(zq[v], tq[v], Qq[v], pass, acc);
     }
   }
 }
 
 __global__ __launch_bounds__(kThreads) void k_trial(Geom g, int pass, const float* zc, const float* tgt,
                                                       const float* Q, const int* found, double* part, int nblk) {
-  __shared__ double red[4][kTrialJ];
   const int q = blockIdx.y;
   if (found[q]) return;
   const int64_t n = g.BT() * g.H;
   const float* zq = zc + (int64_t)q * n;
   const float* tq = tgt + (int64_t)q * n;
   const float* Qq = Q + (int64_t)q * n;
-  float acc[kTrialJ];
+  float acc[kSlots];
 #pragma unroll
-  for (int k = 0; k < kTrialJ; ++k) acc[k] = 0.f;
-  const float scale0 = ldexpf(1.f, -pass * kTrialJ);
+  for (int k = 0; k < kSlots; ++k) acc[k] = 0.f;
   const bool vec = (g.H % 4) == 0;
   if (q == 2) {
-    if (vec) trial_loop<true, 4>(n, zq, tq, Qq, scale0, acc);
-    else trial_loop<true, 1>(n, zq, tq, Qq, scale0, acc);
+    if (vec) trial_loop<true, 4>(n, zq, tq, Qq, pass, acc);
+    else trial_loop<true, 1>(n, zq, tq, Qq, pass, acc);
   } else {
-    if (vec) trial_loop<false, 4>(n, zq, tq, Qq, scale0, acc);
-    else trial_loop<false, 1>(n, zq, tq, Qq, scale0, acc);
+    if (vec) trial_loop<false, 4>(n, zq, tq, Qq, pass, acc);
+    else trial_loop<false, 1>(n, zq, tq, Qq, pass, acc);
   }
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-#pragma unroll
-  for (int k = 0; k < kTrialJ; ++k) {
-    const float s = wave_sum(acc[k]);
-    if (lane == 0) red[w][k] = (double)s;
+  trial_block_store(acc, part, q, nblk);
+}
+
+// Fast trial pass (D <= kFastD, H % 4 == 0): rows x float4 columns.  Side 0 forms the trial
+// direction on the fly, q = x_row . G_x[:, j] (no Q buffer); side 1 applies the x-side
+// update to the cached pre-activations on the fly, z = zc + x_row . dWx[:, j].
+
+struct RowCols {  // thread -> (row offset, float4 column) of a rows x (H/4) grid
+  int tpr, rpb, rr, c4;
+  __device__ RowCols(int H) {
+    const int cols4 = H / 4;
+    tpr = cols4 < kThreads ? cols4 : kThreads;
+    rpb = kThreads / tpr;
+    rr = threadIdx.x / tpr;
+    c4 = threadIdx.x - rr * tpr;
   }
-  __syncthreads();
-  if (threadIdx.x < kTrialJ) {
-    const int k = threadIdx.x;
-    part[((int64_t)q * kTrialJ + k) * nblk + blockIdx.x] = (red[0][k] + red[1][k]) + (red[2][k] + red[3][k]);
+};
+
+template <bool TANH, int SIDE>
+__device__ __forceinline__ void trial_fast_body(const Geom& g, int q, int pass, const float* zc, const float* tgt,
+                                                const float* Q, const float* x, const float* Wlds, float (&acc)[kSlots]) {
+  const int64_t BT = g.BT(), n = BT * g.H;
+  const float* zq = zc + (int64_t)q * n;
+  const float* tq = tgt + (int64_t)q * n;
+  const float* Qq = Q ? Q + (int64_t)q * n : nullptr;
+  RowCols rc(g.H);
+  if (rc.rr >= rc.rpb) return;
+  const int j = 4 * rc.c4;          // fast path: H/4 <= 256, one float4 column per thread
+  for (int64_t row = (int64_t)blockIdx.x * rc.rpb + rc.rr; row < BT; row += (int64_t)gridDim.x * rc.rpb) {
+    const int64_t e = row * g.H + j;
+    float4 z4 = *reinterpret_cast<const float4*>(zq + e);
+    const float4 t4 = *reinterpret_cast<const float4*>(tq + e);
+    float4 w4 = make_float4(0.f, 0.f, 0.f, 0.f);
+    const float* xr = x + row * g.D;
+#pragma unroll 4
+    for (int d = 0; d < g.D; ++d) {
+      const float xd = xr[d];
+      const float4 wv = *reinterpret_cast<const float4*>(Wlds + d * g.H + j);
+      w4.x += xd * wv.x; w4.y += xd * wv.y; w4.z += xd * wv.z; w4.w += xd * wv.w;
+    }
+    float4 q4;
+    if (SIDE == 0) {
+      q4 = w4;
+    } else {
+      z4.x = z4.x + w4.x; z4.y = z4.y + w4.y; z4.z = z4.z + w4.z; z4.w = z4.w + w4.w;
+      q4 = *reinterpret_cast<const float4*>(Qq + e);
+    }
+#pragma unroll 1
+    for (int u = 0; u < 4; ++u) {
+      const float zu = u == 0 ? z4.x : (u == 1 ? z4.y : (u == 2 ? z4.z : z4.w));
+      const float tu = u == 0 ? t4.x : (u == 1 ? t4.y : (u == 2 ? t4.z : t4.w));
+      const float qu = u == 0 ? q4.x : (u == 1 ? q4.y : (u == 2 ? q4.z : q4.w));
+      trial_accumulate<TANH>(zu, tu, qu, pass, acc);
+    }
   }
 }
 
-// Test hook: the same per-element arithmetic on caller data (one gate), partial sums per block.
+// Wsrc: side 0 -> G_x [4][D][H]; side 1 -> dWx [4][D][H]
+template <int SIDE>
+__global__ __launch_bounds__(kThreads) void k_trial_fast(Geom g, int pass, const float* zc, const float* tgt,
+                                                           const float* Q, const float* x, const float* Wsrc,
+                                                           const int* found, double* part, int nblk) {
+  extern __shared__ float wlds[];  // [D][H]
+  const int q = blockIdx.y;
+  if (found[q]) return;
+  const int nW = g.D * g.H;
+  for (int i = threadIdx.x; i < nW; i += kThreads) wlds[i] = Wsrc[(int64_t)q * nW + i];
+  __syncthreads();
+  float acc[kSlots];
+#pragma unroll
+  for (int k = 0; k < kSlots; ++k) acc[k] = 0.f;
+  if (q == 2) trial_fast_body<true, SIDE>(g, q, pass, zc, tgt, Q, x, wlds, acc);
+  else trial_fast_body<false, SIDE>(g, q, pass, zc, tgt, Q, x, wlds, acc);
+  trial_block_store(acc, part, q, nblk);
+}
+
+// x-stage residual fused with G_x = X^T R (admm.py:302-312, x side): per element
+// tgt = lam/rho + S (stored for the trials and the h stage), R = (phi(z) - tgt) phi'(z),
+// and per block the partial sums X^T R into a [D][H] slab (R never reaches HBM).
+__global__ __launch_bounds__(kThreads) void k_resid_gx(Geom g, Hyper hp, const float* x, Planes6 S, Planes6 L,
+                                                         const float* zc, float* tgt, float* slab) {
+  extern __shared__ float gl[];  // [D][H] block accumulator
+  const int q = blockIdx.y;
+  const bool th = (q == 2);
+  const float rho = hp.rho[q];
+  const int64_t BT = g.BT(), n = BT * g.H;
+  const float* zq = zc + (int64_t)q * n;
+  float* tq = tgt + (int64_t)q * n;
+  const float* Sq = S.p[q];
+  const float* Lq = L.p[q];
+  RowCols rc(g.H);                 // fast path: H/4 <= 256, one float4 column per thread
+  const int j = 4 * rc.c4;
+  float acc[kFastD][4];
+#pragma unroll
+  for (int d = 0; d < kFastD; ++d) acc[d][0] = acc[d][1] = acc[d][2] = acc[d][3] = 0.f;
+  const int64_t per_blk = (BT + gridDim.x - 1) / gridDim.x;
+  const int64_t r0 = (int64_t)blockIdx.x * per_blk, r1 = r0 + per_blk < BT ? r0 + per_blk : BT;
+  if (rc.rr < rc.rpb) {
+    for (int64_t row = r0 + rc.rr; row < r1; row += rc.rpb) {
+      const int64_t b = row / g.T;
+      const int64_t so = (row + b + 1) * g.H;  // (b*(T+1) + t) * H with t = row - b*T + 1
+      float xr[kFastD];
+#pragma unroll
+      for (int d = 0; d < kFastD; ++d) xr[d] = d < g.D ? x[row * g.D + d] : 0.f;
+      const float4 z4 = *reinterpret_cast<const float4*>(zq + row * g.H + j);
+      const float4 l4 = *reinterpret_cast<const float4*>(Lq + so + j);
+      const float4 s4 = *reinterpret_cast<const float4*>(Sq + so + j);
+      float4 t4;
+      t4.x = l4.x / rho + s4.x; t4.y = l4.y / rho + s4.y; t4.z = l4.z / rho + s4.z; t4.w = l4.w / rho + s4.w;
+      *reinterpret_cast<float4*>(tq + row * g.H + j) = t4;
+      const float zz[4] = {z4.x, z4.y, z4.z, z4.w}, tt[4] = {t4.x, t4.y, t4.z, t4.w};
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        float phi, dphi;
+        if (th) {
+          phi = tanhf(zz[u]);
+          dphi = 1.f - phi * phi;
+        } else {
+          const SigPair sp = sig_pair(zz[u]);
+          phi = sp.s;
+          dphi = sp.s * sp.sc;
+        }
+        const float R = (phi - tt[u]) * dphi;
+#pragma unroll
+        for (int d = 0; d < kFastD; ++d) acc[d][u] += xr[d] * R;
+      }
+    }
+  }
+  // deterministic in-block combine of the row groups, then one slab per block
+  for (int i = threadIdx.x; i < g.D * g.H; i += kThreads) gl[i] = 0.f;
+  __syncthreads();
+  for (int grp = 0; grp < rc.rpb; ++grp) {
+    if (rc.rr == grp) {
+#pragma unroll
+      for (int d = 0; d < kFastD; ++d) {
+        if (d < g.D) {
+          float* dst = gl + d * g.H + j;
+          dst[0] += acc[d][0]; dst[1] += acc[d][1]; dst[2] += acc[d][2]; dst[3] += acc[d][3];
+        }
+      }
+    }
+    __syncthreads();
+  }
+  float* out = slab + ((int64_t)blockIdx.x * 4 + q) * g.D * g.H;
+  for (int i = threadIdx.x; i < g.D * g.H; i += kThreads) out[i] = gl[i];
+}
+
+// Test hook: the same per-element arithmetic on caller data (one gate), kbase = pass*J:
+// per block the J candidate sums of that window, with the polynomial part already
+// evaluated at s = 2^-(kbase+k), so part[blk][k] is the full increment sum.
 __global__ __launch_bounds__(kThreads) void k_trial_debug(int64_t n, int tanh_gate, int kbase, const float* z,
                                                             const float* tgt, const float* qv, double* part) {
-  __shared__ double red[4][kTrialJ];
-  float acc[kTrialJ];
+  __shared__ double red[4][kSlots];
+  float acc[kSlots];
 #pragma unroll
-  for (int k = 0; k < kTrialJ; ++k) acc[k] = 0.f;
-  const float scale0 = ldexpf(1.f, -kbase);
-  if (tanh_gate) trial_loop<true, 1>(n, z, tgt, qv, scale0, acc);
-  else trial_loop<false, 1>(n, z, tgt, qv, scale0, acc);
+  for (int k = 0; k < kSlots; ++k) acc[k] = 0.f;
+  const int pass = kbase / kTrialJ;
+  // the polynomial slots are only filled on pass 0: run pass 0 for them, then this pass
+  if (tanh_gate) trial_loop<true, 1>(n, z, tgt, qv, 0, acc);
+  else trial_loop<false, 1>(n, z, tgt, qv, 0, acc);
+  if (pass > 0) {
+    float acc2[kSlots];
+#pragma unroll
+    for (int k = 0; k < kSlots; ++k) acc2[k] = 0.f;
+    if (tanh_gate) trial_loop<true, 1>(n, z, tgt, qv, pass, acc2);
+    else trial_loop<false, 1>(n, z, tgt, qv, pass, acc2);
+#pragma unroll
+    for (int k = 0; k < kTrialJ; ++k) acc[k] = acc2[k];
+  }
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
 #pragma unroll
-  for (int k = 0; k < kTrialJ; ++k) {
+  for (int k = 0; k < kSlots; ++k) {
     const float s = wave_sum(acc[k]);
     if (lane == 0) red[w][k] = (double)s;
   }
   __syncthreads();
   if (threadIdx.x < kTrialJ) {
     const int k = threadIdx.x;
-    part[(int64_t)blockIdx.x * kTrialJ + k] = (red[0][k] + red[1][k]) + (red[2][k] + red[3][k]);
+    double tot[kSlots];
+    for (int i = 0; i < kSlots; ++i) tot[i] = (red[0][i] + red[1][i]) + (red[2][i] + red[3][i]);
+    const double sk = ldexp(1.0, -(kbase + k));
+    double poly = 0.0;
+    for (int n2 = kPolyN - 1; n2 >= 0; --n2) poly = (poly + tot[kSlotPoly + n2]) * sk;
+    part[(int64_t)blockIdx.x * kTrialJ + k] = tot[k] + poly;
   }
 }
 
-__global__ __launch_bounds__(kThreads) void k_trial_reduce(int pass, const double* part, int nblk,
-                                                             const double* fw_part, int fw_nblk, const int* found,
+__global__ __launch_bounds__(kThreads) void k_trial_reduce(int pass, const double* part, int nblk, const int* found,
                                                              double* sums) {
   __shared__ double red[4];
   const int q = blockIdx.x;
   if (found[q]) return;
-  for (int k = 0; k <= kTrialJ; ++k) {
+  for (int k = 0; k < kSlots; ++k) {
     double s = 0.0;
-    if (k < kTrialJ) {
-      const double* p = part + ((int64_t)q * kTrialJ + k) * nblk;
-      for (int i = threadIdx.x; i < nblk; i += kThreads) s += p[i];
-    } else {
-      const double* p = fw_part + (int64_t)q * fw_nblk;
-      for (int i = threadIdx.x; i < fw_nblk; i += kThreads) s += p[i];
-    }
+    const double* p = part + ((int64_t)q * kSlots + k) * nblk;
+    for (int i = threadIdx.x; i < nblk; i += kThreads) s += p[i];
     const double tot = block_sum(s, red);
-    if (threadIdx.x == 0) sums[q * (kTrialJ + 1) + k] = tot;
+    if (threadIdx.x == 0) sums[q * kSlots + k] = tot;
   }
 }
 
-// First k of this window with f(W + G/2^k) <= est_k (admm.py:331-336); then
+// First k with f(W + G/2^k) <= est_k (admm.py:331-336); then
 // W <- (0.5 rho T theta* W - G) / (beta + 0.5 rho theta* T), theta* = 2^k / 2 (admm.py:338-343).
+// lhs_k = 0.5 rho (per-candidate sum of this window + polynomial part at s = 2^-k);
+// rhs_k = est_k - f(W) = sum G (beta - W) + 0.5 T theta ||beta - W||^2 = (1 + T/2) ||G||^2 2^-k.
+// If every element was in the polynomial regime the decision extends over all k < kMaxK.
 __global__ __launch_bounds__(kThreads) void k_select(Geom g, Hyper hp, SelectArgs a) {
   __shared__ double red[4];
   __shared__ int pick_s;
@@ -470,25 +885,33 @@ __global__ __launch_bounds__(kThreads) void k_select(Geom g, Hyper hp, SelectArg
   const double gsq = block_sum(gs, red);
   const float rho = hp.rho[q];
   if (threadIdx.x == 0) {
-    const double* sm = a.sums + q * (kTrialJ + 1);
+    const double* sm = a.sums + q * kSlots;
+    if (a.pass == 0)
+      for (int n = 0; n < kPolyN; ++n) a.poly[q * kPolyN + n] = sm[kSlotPoly + n];
+    const bool poly_only = sm[kSlotNne] == 0.0;
+    const int k_lo = poly_only ? 0 : a.pass * kTrialJ;
+    const int k_hi = poly_only ? kMaxK : k_lo + kTrialJ;
     int pick = -1;
-    for (int k = 0; k < kTrialJ; ++k) {
-      const int kk = a.pass * kTrialJ + k;
-      const double lhs = 0.5 * (double)rho * sm[k];
-      const double rhs = (1.0 + 0.5 * g.T) * gsq * ldexp(1.0, -kk);
+    for (int kk = k_lo; kk < k_hi; ++kk) {
+      const double sk = ldexp(1.0, -kk);
+      double poly = 0.0;
+      for (int n = kPolyN - 1; n >= 0; --n) poly = (poly + a.poly[q * kPolyN + n]) * sk;
+      const double cand = poly_only ? 0.0 : sm[kk - k_lo];
+      const double lhs = 0.5 * (double)rho * (cand + poly);
+      const double rhs = (1.0 + 0.5 * g.T) * gsq * sk;
       if (!isfinite(lhs)) atomicAdd(&a.stats->nonfinite, 1);
       if (lhs > rhs) continue;
       pick = kk;
       break;
     }
-    if (pick < 0 && a.pass == a.last_pass) {
-      pick = (a.last_pass + 1) * kTrialJ;
+    if (pick < 0 && (poly_only || a.pass == a.last_pass)) {
+      pick = k_hi;
       atomicAdd(&a.stats->unresolved, 1);
     }
     if (pick >= 0) {
       const int slot = 2 * q + a.side;
       a.stats->k[slot] = pick;
-      a.stats->f_w[slot] = 0.5 * (double)rho * sm[kTrialJ];
+      a.stats->f_w[slot] = 0.5 * (double)rho * sm[kSlotFw];
       a.stats->grad_sq[slot] = gsq;
       a.stats->passes[a.side] = a.pass + 1;
       a.found[q] = 1;
@@ -744,14 +1167,19 @@ __global__ __launch_bounds__(kThreads) void k_ht_apply(Geom g, Hyper hp, Planes6
 
 // ============================================================================ launchers
 
+// float4 staging needs 16-byte aligned rows of x and of the [.., H] planes
+inline int vec_ok(const Geom& g) { return (g.D % 4 == 0 && g.H % 4 == 0) ? 1 : 0; }
+
 void launch_forward_t(const Geom& g, int t, const Weights& w, const ForwardT& a, hipStream_t s) {
-  dim3 grid(cdiv64(g.B, TS_BM), cdiv64(g.H, 32));
-  k_forward_t<<<grid, kThreads, 0, s>>>(g, t, w, a);
+  dim3 grid(cdiv64(g.B, TS_BM) * cdiv64(g.H, 32));
+  if (vec_ok(g) && (a.hprev_stride % 4 == 0)) k_forward_t<true><<<grid, kThreads, 0, s>>>(g, t, w, a);
+  else k_forward_t<false><<<grid, kThreads, 0, s>>>(g, t, w, a);
 }
 
 void launch_sweep_t(const Geom& g, int t, const Weights& w, const Hyper& hp, const SweepT& a, hipStream_t s) {
-  dim3 grid(cdiv64(g.B, TS_BM), cdiv64(g.H, 32));
-  k_sweep_t<<<grid, kThreads, 0, s>>>(g, t, w, hp, a);
+  dim3 grid(cdiv64(g.B, TS_BM) * cdiv64(g.H, 32));
+  if (vec_ok(g)) k_sweep_t<true><<<grid, kThreads, 0, s>>>(g, t, w, hp, a);
+  else k_sweep_t<false><<<grid, kThreads, 0, s>>>(g, t, w, hp, a);
 }
 
 void launch_rowdot(int64_t B, int H, int O, const float* h, int64_t hs, const float* wy, float* out, hipStream_t s) {
@@ -761,8 +1189,9 @@ void launch_rowdot(int64_t B, int H, int O, const float* h, int64_t hs, const fl
 }
 
 void launch_zgemm(const Geom& g, const Weights& w, const float* x, const float* Sh, float* zc, hipStream_t s) {
-  dim3 grid(cdiv64(g.BT(), TS_BM), cdiv64(g.H, 32));
-  k_zgemm<<<grid, kThreads, 0, s>>>(g, w, x, Sh, zc);
+  dim3 grid(cdiv64(g.BT(), TS_BM) * cdiv64(g.H, 32));
+  if (vec_ok(g)) k_zgemm<true><<<grid, kThreads, 0, s>>>(g, w, x, Sh, zc);
+  else k_zgemm<false><<<grid, kThreads, 0, s>>>(g, w, x, Sh, zc);
 }
 
 int resid_blocks(const Geom& g) {
@@ -779,7 +1208,7 @@ void launch_resid(const Geom& g, const Hyper& hp, const ResidArgs& a, hipStream_
 
 int atr_splits(const Geom& g, int side) {
   const int Kd = side == 0 ? g.D : g.H;
-  const int tiles = cdiv64(Kd, AT_BM) * cdiv64(g.H, AT_BN) * 4;
+  const int tiles = cdiv64(Kd, side == 1 ? 128 : 32) * cdiv64(g.H, 128) * 4;
   int ns = 1024 / tiles;
   const int64_t max_by_rows = g.BT() / 256;  // keep >= 256 rows per split
   if (ns > max_by_rows) ns = (int)max_by_rows;
@@ -790,8 +1219,14 @@ int atr_splits(const Geom& g, int side) {
 void launch_atr(const Geom& g, int side, const float* x, const float* Sh, const float* R, float* slab, int nsplit,
                 hipStream_t s) {
   const int Kd = side == 0 ? g.D : g.H;
-  dim3 grid(cdiv64(Kd, AT_BM), cdiv64(g.H, AT_BN), 4 * nsplit);
-  k_atr<<<grid, kThreads, 0, s>>>(g, side, x, Sh, R, slab, nsplit);
+  dim3 grid(cdiv64(Kd, side == 1 ? 128 : 32) * cdiv64(g.H, 128) * 4 * nsplit);
+  if (side == 1) {
+    if (vec_ok(g)) k_atr<128, 64, true><<<grid, kThreads, 0, s>>>(g, side, x, Sh, R, slab, nsplit);
+    else k_atr<128, 64, false><<<grid, kThreads, 0, s>>>(g, side, x, Sh, R, slab, nsplit);
+  } else {
+    if (vec_ok(g)) k_atr<32, 32, true><<<grid, kThreads, 0, s>>>(g, side, x, Sh, R, slab, nsplit);
+    else k_atr<32, 32, false><<<grid, kThreads, 0, s>>>(g, side, x, Sh, R, slab, nsplit);
+  }
 }
 
 void launch_reduce_g(const Geom& g, int side, const Hyper& hp, const float* slab, int nsplit, float* G,
@@ -803,8 +1238,9 @@ void launch_reduce_g(const Geom& g, int side, const Hyper& hp, const float* slab
 
 void launch_qgemm(const Geom& g, int side, const float* x, const float* Sh, const float* G, float* Q,
                   hipStream_t s) {
-  dim3 grid(cdiv64(g.BT(), TS_BM), cdiv64(g.H, 32));
-  k_qgemm<<<grid, kThreads, 0, s>>>(g, side, x, Sh, G, Q);
+  dim3 grid(cdiv64(g.BT(), TS_BM) * cdiv64(g.H, 32));
+  if (vec_ok(g)) k_qgemm<true><<<grid, kThreads, 0, s>>>(g, side, x, Sh, G, Q);
+  else k_qgemm<false><<<grid, kThreads, 0, s>>>(g, side, x, Sh, G, Q);
 }
 
 int trial_blocks(const Geom& g) {
@@ -823,10 +1259,40 @@ void launch_trial_debug(int64_t n, int tanh_gate, int kbase, const float* z, con
   k_trial_debug<<<nblk, kThreads, 0, s>>>(n, tanh_gate, kbase, z, tgt, q, part);
 }
 
-void launch_trial_reduce(const Geom& g, int pass, const double* part, int nblk, const double* fw_part, int fw_nblk,
-                         const int* found, double* sums, hipStream_t s) {
+void launch_trial_reduce(const Geom& g, int pass, const double* part, int nblk, const int* found, double* sums,
+                         hipStream_t s) {
   (void)g;
-  k_trial_reduce<<<4, kThreads, 0, s>>>(pass, part, nblk, fw_part, fw_nblk, found, sums);
+  k_trial_reduce<<<4, kThreads, 0, s>>>(pass, part, nblk, found, sums);
+}
+
+bool fast_path(const Geom& g) {
+  return g.D <= kFastD && g.H % 4 == 0 && g.H / 4 <= kThreads && (int64_t)g.D * g.H * 4 <= 64 * 1024;
+}
+
+int resid_gx_blocks(const Geom& g) {
+  int nb = cdiv64(g.BT(), 256);
+  return nb > 256 ? 256 : (nb < 1 ? 1 : nb);
+}
+
+void launch_resid_gx(const Geom& g, const Hyper& hp, const float* x, const Planes6& S, const Planes6& L,
+                     const float* zc, float* tgt, float* slab, int nblk, hipStream_t s) {
+  dim3 grid(nblk, 4);
+  k_resid_gx<<<grid, kThreads, (size_t)g.D * g.H * sizeof(float), s>>>(g, hp, x, S, L, zc, tgt, slab);
+}
+
+void launch_atr_fused(const Geom& g, const Hyper& hp, const float* x, const float* Sh, const float* zc,
+                      const float* tgt, const float* dW, float* slab, int nsplit, hipStream_t s) {
+  (void)hp;
+  dim3 grid(cdiv64(g.H, 128) * cdiv64(g.H, 128) * 4 * nsplit);
+  k_atr_fused<<<grid, kThreads, 0, s>>>(g, x, Sh, zc, tgt, dW, slab, nsplit);
+}
+
+void launch_trial_fast(const Geom& g, int side, int pass, const float* zc, const float* tgt, const float* Q,
+                       const float* x, const float* Wsrc, const int* found, double* part, int nblk, hipStream_t s) {
+  dim3 grid(nblk, 4);
+  const size_t lds = (size_t)g.D * g.H * sizeof(float);
+  if (side == 0) k_trial_fast<0><<<grid, kThreads, lds, s>>>(g, pass, zc, tgt, Q, x, Wsrc, found, part, nblk);
+  else k_trial_fast<1><<<grid, kThreads, lds, s>>>(g, pass, zc, tgt, Q, x, Wsrc, found, part, nblk);
 }
 
 void launch_select(const Geom& g, const Hyper& hp, const SelectArgs& a, hipStream_t s) {

@@ -7,7 +7,12 @@
 namespace admm {
 
 constexpr int kTrialJ = 16;      // line-search candidates evaluated per trial pass
+// per-gate sums of a trial pass: [J candidates][6 polynomial coefficients][sum d0^2][#per-candidate elements]
+constexpr int kPolyN = 6;
+constexpr int kTrialSlots = kTrialJ + kPolyN + 2;
+constexpr int kMaxK = 96;        // exponents decided from the polynomial alone go up to this
 constexpr int kMaxPasses = 4;    // => exponents k in [0, 64)
+constexpr int kFastD = 16;       // fused weight-stage path for input_size <= 16
 constexpr int kHTCand = 4;       // theta = 0.1, 0.2, 0.4, 0.8 (admm.py:447-480)
 constexpr int kHTSums = 1 + 3 * kHTCand;
 
@@ -80,7 +85,6 @@ struct ResidArgs {
   float* tgt;               // written (stage 0) / read (stage 1); [4][BT][H] = L/rho + S
   float* R;                 // [4][BT][H] residual (phi(z) - tgt) * phi'(z)
   const float* dW;          // [4][D][H] (stage 1)
-  double* fw_part;          // [4][nblk]
   int nblk;
 };
 int resid_blocks(const Geom& g);
@@ -104,14 +108,28 @@ void launch_trial(const Geom& g, int pass, const float* zc, const float* tgt, co
 // test hook: part[blk][J] for caller-provided z, tgt, q of one gate
 void launch_trial_debug(int64_t n, int tanh_gate, int kbase, const float* z, const float* tgt, const float* q,
                         double* part, int nblk, hipStream_t s);
-// sums[q][0..J) = sum_blk part ; sums[q][J] = f(W) partial sum
-void launch_trial_reduce(const Geom& g, int pass, const double* part, int nblk, const double* fw_part,
-                         int fw_nblk, const int* found, double* sums, hipStream_t s);
+// sums[q][0..J) = sum_blk part[q][k] ; sums[q][J] = sum d0^2 (= 2 f(W)/rho)
+void launch_trial_reduce(const Geom& g, int pass, const double* part, int nblk, const int* found, double* sums,
+                         hipStream_t s);
+
+// ---- fast weight-stage path (D <= 16, H % 4 == 0): fused residual/gradient kernels
+bool fast_path(const Geom& g);
+int resid_gx_blocks(const Geom& g);
+// x stage: tgt = lam/rho + S (stored) and slab[blk][q][d][j] = sum_rows x[row][d] R_q[row][j]
+void launch_resid_gx(const Geom& g, const Hyper& hp, const float* x, const Planes6& S, const Planes6& L,
+                     const float* zc, float* tgt, float* slab, int nblk, hipStream_t s);
+// trial pass without a materialised Q (side 0: q = x.G_x) or z (side 1: z = zc + x.dWx)
+void launch_trial_fast(const Geom& g, int side, int pass, const float* zc, const float* tgt, const float* Q,
+                       const float* x, const float* Wsrc, const int* found, double* part, int nblk, hipStream_t s);
+// h stage A^T R with R computed on the fly from zc, tgt, x, dWx (side 1, fast path)
+void launch_atr_fused(const Geom& g, const Hyper& hp, const float* x, const float* Sh, const float* zc,
+                      const float* tgt, const float* dW, float* slab, int nsplit, hipStream_t s);
 // decide the first passing k in this pass's window; on success update the weights
 struct SelectArgs {
   int side;                 // 0 x, 1 h
   int pass, last_pass;
-  const double* sums;       // [4][J+1]
+  const double* sums;       // [4][kTrialSlots] of this pass
+  double* poly;             // [4][kPolyN] polynomial coefficients kept from pass 0
   const float* G;           // [4][K][H]
   float* W[4];              // weights being updated (in place)
   float* dW;                // [4][K][H] W_new - W_old (side 0), nullable

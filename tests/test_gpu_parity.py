@@ -7,8 +7,8 @@ Tolerances (north_star: per-iteration loss within 1e-5 relative, fp32):
   (gates are in [-1, 1]; fp32 eps ~ 6e-8);
 * line-search exponents: the reference's fp32 comparisons at large theta are rounding
   noise (DESIGN.md "line-search numerics"); the HIP path decides on accurate increments,
-  so it is checked against an fp64 run of the oracle instead: identical wherever the
-  fp64 decision margin exceeds 5 %, otherwise within one doubling.
+  so it is checked against an fp64 oracle step taken from the GPU's own state instead:
+  identical wherever the fp64 decision margin exceeds 1 %, otherwise within one doubling.
 """
 import ctypes
 import importlib.util
@@ -59,28 +59,25 @@ def _loss(model, x, y):
     return float(torch.nn.functional.mse_loss(model(x), y))
 
 
-def _fp64_decisions(g: Golden, steps):
-    """Per step, per weight search: (k, margin) of an fp64 oracle run from the same initial
-    state.  margin = smallest |f(beta) - est| / |est - f(W)| of the deciding comparisons
-    (the last failing one and the passing one)."""
+def _fp64_step_decisions(g: Golden, W, S, L):
+    """(k, margin) of each weight search of ONE fp64 oracle step from the given fp32 state.
+    margin = smallest |f(beta) - est| / |est - f(W)| of the deciding comparisons (the last
+    failing one and the passing one)."""
     torch.set_default_dtype(torch.float64)
     orig = O._autograd
     try:
         hp = O.Hyper.from_dict(g.params, g.variant, g.with_dual_y)
         hp.rho = {k: v.double() for k, v in hp.rho.items()}
         hp.beta = {k: v.double() for k, v in hp.beta.items()}
-        st = O.init_state(g.x.double(), g.y.double(), {k: v.double() for k, v in g.weights(0).items()})
+        d = lambda m: {k: v.double().cpu() for k, v in m.items()}  # noqa: E731
+        st = O.State(g.x.double(), g.y.double(), d(W), d(S), d(L), g.B)
         O._autograd = lambda fn, at: (lambda v: (fn(v).backward(), v.grad)[1])(
             at.clone().detach().requires_grad_(True))
-        stp = O.Stepper(hp, trace_fw=True)
-        out = []
-        for _ in range(steps):
-            dec = []
-            for r in stp.step(st)['weights']:
-                ms = [abs(a - b) / abs(b - r['f_w']) for a, b, _ in r['tests'][-2:] if b != r['f_w']]
-                dec.append((r['k'], min(ms) if ms else math.inf))
-            out.append(dec)
-        return out
+        dec = []
+        for r in O.Stepper(hp, trace_fw=True).step(st)['weights']:
+            ms = [abs(a - b) / abs(b - r['f_w']) for a, b, _ in r['tests'][-2:] if b != r['f_w']]
+            dec.append((r['k'], min(ms) if ms else math.inf))
+        return dec
     finally:
         O._autograd = orig
         torch.set_default_dtype(torch.float32)
@@ -129,26 +126,49 @@ def test_teacher_forced_steps(name, mods, dev):
         assert _loss(model, x, y) == pytest.approx(g.losses[k + 1], rel=LOSS_RTOL)
 
 
-@pytest.mark.parametrize('name', ['t0_admm', 't0_uniform', 't0_yahoo', 't3_tf', 't2_c2'])
-def test_line_search_matches_fp64_oracle(name, mods, dev):
-    """Exponents equal the fp64 oracle's wherever its decision margin exceeds 5 % (fp32
-    state noise moves G by ~1e-3 relative at near-consistent states); elsewhere within
-    one doubling."""
-    g = Golden(name)
-    steps = min(g.steps, 4)
-    ref = _fp64_decisions(g, steps)
-    model, opt = _optimizer(g, mods, dev)
+@pytest.mark.parametrize('shape,variant', [((256, 6, 4, 32), 'admm'), ((300, 5, 16, 48), 'admm'),
+                                           ((200, 8, 1, 12), 'no_dual_y'), ((512, 4, 8, 64), 'admm')])
+def test_line_search_matches_fp64_oracle(shape, variant, mods, dev):
+    """From a perturbed state (the consistent initial state plus 1e-2 noise on gates and
+    duals: weight gradients well above fp32 rounding), one GPU step vs one fp64 oracle
+    step from the identical state: the eight line-search exponents agree wherever the
+    fp64 decision margin exceeds 1 % (else within one doubling)."""
+    from blocks.lstm import LSTM
+    from parameters import example_parameter_dictionary
+    admm, nd = mods
+    admm.with_dual_y = False
+    B, T, D, H = shape
+    gen = torch.Generator().manual_seed(11)
+    x = torch.rand(B, T, D, generator=gen)
+    y = torch.rand(B, 1, generator=gen)
+    pd = example_parameter_dictionary['GoogleStock']
+    torch.manual_seed(0)
+    model = LSTM(D, H, 1)
+    mod = admm if variant == 'admm' else nd
+    opt = mod.ADMMBasedOptimizer(model, (x.to(dev), y.to(dev)), pd, verbose=False)
+    with torch.no_grad():
+        for q in GATES6:
+            noise = 1e-2 * torch.randn(B, T + 1, H, generator=gen)
+            noise[:, 0] = 0
+            opt.gates[q].add_(noise.to(dev))
+            if q != 'h':
+                opt.duals[q].copy_(1e-2 * torch.randn(B, T + 1, H, generator=gen))
+    W = {n: p.detach().clone() for n, p in model.named_parameters()}
+    S = {k: v.clone() for k, v in opt.gates.items()}
+    L = {k: v.clone() for k, v in opt.duals.items()}
+    g = type('G', (), dict(params=pd, variant=variant, with_dual_y=False, x=x, y=y, B=B))
+    ref = _fp64_step_decisions(g, W, S, L)
+    opt.step()
+    ks = list(opt.last_step_stats()['k'].values())
     clear = 0
-    for s in range(steps):
-        opt.step()
-        ks = list(opt.last_step_stats()['k'].values())
-        for a, (b, margin) in zip(ks, ref[s]):
-            if margin > 0.05:
-                clear += 1
-                assert a == b, (s, ks, ref[s])
-            else:
-                assert abs(a - b) <= 1, (s, ks, ref[s])
-    assert clear >= steps * 4
+    for a, (b, margin) in zip(ks, ref):
+        if margin > 0.01:
+            clear += 1
+            assert a == b, (ks, ref)
+        else:
+            assert abs(a - b) <= 1, (ks, ref)
+    assert clear >= 6, ref
+    assert sum(k > 0 for k, _ in ref) >= 4, ref   # the searches actually iterate
 
 
 @pytest.mark.parametrize('tanh_gate', [0, 1])

@@ -151,14 +151,17 @@ __device__ __forceinline__ T block_sum(T v, T* red /* >= 4 entries of LDS */) {
 //   a4(m, k), b4(k, n): float4 at (m, k) / (k, n); zero outside the problem.
 //   B is always [k][n] -> float4 = 4 consecutive n.
 
-template <int BM, int BN, int WM, int WN, int KC>
+template <int BM, int BN, int WM, int WN, int KC, bool A_ROW = false>
 struct Tile {
   static constexpr int MT = WM / 32, NT = WN / 32;
   static constexpr int WAVES_N = BN / WN;
   static_assert((BM / WM) * (BN / WN) == 4, "4 waves per workgroup");
-  static_assert(KC % 4 == 0 && BM % 4 == 0 && BN % 4 == 0, "float4 staging");
-  static constexpr int AS = BM + 4, BS = BN + 4;     // LDS row strides (dwords)
-  static constexpr int STAGE_FLOATS = KC * AS + KC * BS;
+  static_assert(KC % 8 == 0 && BM % 4 == 0 && BN % 4 == 0, "float4 staging");
+  // A image: A_ROW -> As[m][KC+4] (rows 16-byte aligned; ds_read_b128 of 4 consecutive k is
+  // conflict-free since (KC+4)/4 is odd); else As[k][BM+4].  B image: Bs[k][BN+4].
+  static constexpr int AS = A_ROW ? KC + 4 : BM + 4, BS = BN + 4;
+  static constexpr int A_FLOATS = A_ROW ? BM * AS : KC * AS;
+  static constexpr int STAGE_FLOATS = A_FLOATS + KC * BS;
   static constexpr int LDS_FLOATS = 2 * STAGE_FLOATS;  // double-buffered
   static constexpr int A4 = BM * KC / 4, B4 = BN * KC / 4;
   static constexpr int A_PER = (A4 + kThreads - 1) / kThreads, B_PER = (B4 + kThreads - 1) / kThreads;
@@ -179,7 +182,7 @@ __device__ __forceinline__ int acc_row(int r, int lane) { return (r & 3) + 8 * (
 
 template <int BM, int BN, int WM, int WN, int KC, class P>
 struct Engine {
-  using S = Tile<BM, BN, WM, WN, KC>;
+  using S = Tile<BM, BN, WM, WN, KC, P::A_ROW_MAJOR>;
   float4 ra[S::A_PER], rb[S::B_PER];
 
   __device__ __forceinline__ void load(const P& p, int64_t m0, int64_t n0, int64_t kb) {
@@ -205,16 +208,10 @@ struct Engine {
     for (int i = 0; i < S::A_PER; ++i) {
       const int f = tid + i * kThreads;
       if (f < S::A4) {
-        if (P::A_ROW_MAJOR) {
-          const int m = f / (KC / 4), k = 4 * (f % (KC / 4));
-          As[(k + 0) * S::AS + m] = ra[i].x;
-          As[(k + 1) * S::AS + m] = ra[i].y;
-          As[(k + 2) * S::AS + m] = ra[i].z;
-          As[(k + 3) * S::AS + m] = ra[i].w;
-        } else {
-          const int m = 4 * (f % (BM / 4)), k = f / (BM / 4);
-          *reinterpret_cast<float4*>(&As[k * S::AS + m]) = ra[i];
-        }
+        if (P::A_ROW_MAJOR)
+          *reinterpret_cast<float4*>(&As[(f / (KC / 4)) * S::AS + 4 * (f % (KC / 4))]) = ra[i];
+        else
+          *reinterpret_cast<float4*>(&As[(f / (BM / 4)) * S::AS + 4 * (f % (BM / 4))]) = ra[i];
       }
     }
 #pragma unroll
@@ -229,18 +226,43 @@ struct Engine {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int wm0 = (wave / S::WAVES_N) * WM, wn0 = (wave % S::WAVES_N) * WN;
     const int kh = lane >> 5, c = lane & 31;
+    if (P::A_ROW_MAJOR) {
+      // k-permuted: within each 8-k block, MFMA j uses k = {j (lanes 0-31), 4 + j (lanes 32-63)},
+      // so one ds_read_b128 of A[m][8b + 4kh .. +3] feeds 4 MFMAs; B rows follow the same map.
 #pragma unroll
-    for (int kk = 0; kk < KC; kk += 2) {
-      float av[S::MT], bv[S::NT];
+      for (int kb = 0; kb < KC; kb += 8) {
+        float4 a4[S::MT];
 #pragma unroll
-      for (int mi = 0; mi < S::MT; ++mi) av[mi] = As[(kk + kh) * S::AS + wm0 + mi * 32 + c];
+        for (int mi = 0; mi < S::MT; ++mi)
+          a4[mi] = *reinterpret_cast<const float4*>(&As[(wm0 + mi * 32 + c) * S::AS + kb + 4 * kh]);
 #pragma unroll
-      for (int ni = 0; ni < S::NT; ++ni) bv[ni] = Bs[(kk + kh) * S::BS + wn0 + ni * 32 + c];
+        for (int j = 0; j < 4; ++j) {
+          float bv[S::NT];
 #pragma unroll
-      for (int mi = 0; mi < S::MT; ++mi)
+          for (int ni = 0; ni < S::NT; ++ni) bv[ni] = Bs[(kb + 4 * kh + j) * S::BS + wn0 + ni * 32 + c];
 #pragma unroll
-        for (int ni = 0; ni < S::NT; ++ni)
-          acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[mi], bv[ni], acc[mi][ni], 0, 0, 0);
+          for (int mi = 0; mi < S::MT; ++mi) {
+            const float av = j == 0 ? a4[mi].x : (j == 1 ? a4[mi].y : (j == 2 ? a4[mi].z : a4[mi].w));
+#pragma unroll
+            for (int ni = 0; ni < S::NT; ++ni)
+              acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv[ni], acc[mi][ni], 0, 0, 0);
+          }
+        }
+      }
+    } else {
+#pragma unroll
+      for (int kk = 0; kk < KC; kk += 2) {
+        float av[S::MT], bv[S::NT];
+#pragma unroll
+        for (int mi = 0; mi < S::MT; ++mi) av[mi] = As[(kk + kh) * S::AS + wm0 + mi * 32 + c];
+#pragma unroll
+        for (int ni = 0; ni < S::NT; ++ni) bv[ni] = Bs[(kk + kh) * S::BS + wn0 + ni * 32 + c];
+#pragma unroll
+        for (int mi = 0; mi < S::MT; ++mi)
+#pragma unroll
+          for (int ni = 0; ni < S::NT; ++ni)
+            acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[mi], bv[ni], acc[mi][ni], 0, 0, 0);
+      }
     }
   }
 
@@ -251,17 +273,17 @@ struct Engine {
                                       f32x16 (&acc)[S::MT][S::NT], float* smem) {
     if (k0 >= k1) return;
     load(p, m0, n0, k0);
-    store(smem, smem + KC * S::AS);
+    store(smem, smem + S::A_FLOATS);
     __syncthreads();
     int stage = 0;
     for (int64_t kb = k0; kb < k1; kb += KC) {
       const bool more = kb + KC < k1;
       if (more) load(p, m0, n0, kb + KC);
       float* cur = smem + stage * S::STAGE_FLOATS;
-      compute(cur, cur + KC * S::AS, acc);
+      compute(cur, cur + S::A_FLOATS, acc);
       if (more) {
         float* nxt = smem + (stage ^ 1) * S::STAGE_FLOATS;
-        store(nxt, nxt + KC * S::AS);
+        store(nxt, nxt + S::A_FLOATS);
       }
       __syncthreads();
       stage ^= 1;

@@ -169,6 +169,10 @@ int stage_weights(AdmmCtx* c, int side, hipStream_t s) {
   const bool fast = fast_path(g);
   const Planes6 S = planes(c->buf.gates), L = planes(c->buf.duals);
   HIP_TRY(hipMemsetAsync(c->found, 0, 4 * sizeof(int), s));
+  if (fast && side == 1) {  // z of the h-side searches uses the updated x2q (admm.py:298-300)
+    ProfScope ps(c, ADMM_PROF_RESID, s);
+    launch_apply_dwx(g, c->buf.x, c->dW, c->zc, s);
+  }
   int ns;
   // 1. G_q = rho_q sum_rows A^T R_q
   if (fast && side == 0) {
@@ -217,16 +221,17 @@ int stage_weights(AdmmCtx* c, int side, hipStream_t s) {
   sa.dW = side == 0 ? c->dW : nullptr;
   sa.found = c->found;
   sa.stats = c->stats;
+  const int nblk = fast ? stream_blocks(g) : c->nblk_trial;
   for (int pass = 0; pass < kMaxPasses; ++pass) {
     {
       ProfScope ps(c, pass == 0 ? ADMM_PROF_TRIAL : ADMM_PROF_TRIAL_EXTRA, s);
       if (fast)
         launch_trial_fast(g, side, pass, c->zc, c->tgt, side == 1 ? c->Q : nullptr, c->buf.x,
-                          side == 0 ? c->G : c->dW, c->found, c->tr_part, c->nblk_trial, s);
+                          side == 0 ? c->G : c->dW, c->found, c->tr_part, nblk, s);
       else
-        launch_trial(g, pass, c->zc, c->tgt, c->Q, c->found, c->tr_part, c->nblk_trial, s);
+        launch_trial(g, pass, c->zc, c->tgt, c->Q, c->found, c->tr_part, nblk, s);
     }
-    launch_trial_reduce(g, pass, c->tr_part, c->nblk_trial, c->found, c->tr_sums, s);
+    launch_trial_reduce(g, pass, c->tr_part, nblk, c->found, c->tr_sums, s);
     rc = allreduce_f64(c, c->tr_sums, 4 * kTrialSlots, s);
     if (rc) return rc;
     sa.pass = pass;
@@ -312,7 +317,7 @@ int admm_create(const AdmmDims* dims, const AdmmParams* params, int device, Admm
   const size_t plane = (size_t)g.BT() * g.H;
   const int Kmax = g.D > g.H ? g.D : g.H;
   c->nblk_resid = resid_blocks(g);
-  c->nblk_trial = trial_blocks(g);
+  c->nblk_trial = std::max(trial_blocks(g), stream_blocks(g));
   c->nblk_rx = resid_gx_blocks(g);
   size_t slab = (size_t)atr_splits(g, 0) * 4 * g.D * g.H;
   slab = std::max(slab, (size_t)atr_splits(g, 1) * 4 * g.H * g.H);

@@ -21,7 +21,7 @@ inline int cdiv64(int64_t a, int64_t b) { return (int)((a + b - 1) / b); }
 // rows x all 4 gates, so gate q's pre-activation of (b, j) sits in the same lane for every
 // q and the element-wise ADMM updates run straight out of the accumulators.
 constexpr int TS_BM = 128, TS_BN = 128, TS_WM = 32, TS_WN = 128, TS_KC = 32;
-using TSTile = Tile<TS_BM, TS_BN, TS_WM, TS_WN, TS_KC>;
+using TSTile = Tile<TS_BM, TS_BN, TS_WM, TS_WN, TS_KC, true>;
 
 __device__ __forceinline__ const float* pick4(const float* const (&p)[4], int q) {
   return q == 0 ? p[0] : (q == 1 ? p[1] : (q == 2 ? p[2] : p[3]));
@@ -340,7 +340,7 @@ template <int BM, int WM, bool VEC>
 __device__ __forceinline__ void atr_body(const Geom& g, int side, const float* x, const float* Sh, const float* R,
                                          float* slab, int nsplit, float* smem) {
   constexpr int BN = 128, WN = (BM == 128) ? 64 : 32, KC = 32;
-  using S = Tile<BM, BN, WM, WN, KC>;
+  using S = Tile<BM, BN, WM, WN, KC, false>;
   const int Kd = side == 0 ? g.D : g.H;
   const int nm = (Kd + BM - 1) / BM, nn = (g.H + BN - 1) / BN;
   int lid = xcd_swizzle(blockIdx.x, gridDim.x);
@@ -376,7 +376,7 @@ __device__ __forceinline__ void atr_body(const Geom& g, int side, const float* x
 template <int BM, int WM, bool VEC>
 __global__ __launch_bounds__(kThreads) void k_atr(Geom g, int side, const float* x, const float* Sh,
                                                     const float* R, float* slab, int nsplit) {
-  __shared__ float smem[Tile<BM, 128, WM, (BM == 128) ? 64 : 32, 32>::LDS_FLOATS];
+  __shared__ float smem[Tile<BM, 128, WM, (BM == 128) ? 64 : 32, 32, false>::LDS_FLOATS];
   atr_body<BM, WM, VEC>(g, side, x, Sh, R, slab, nsplit, smem);
 }
 
@@ -384,9 +384,9 @@ __global__ __launch_bounds__(kThreads) void k_atr(Geom g, int side, const float*
 // z = zc + x_row . dWx (the x-side update, already applied to the weights), then
 // R = (phi(z) - tgt) phi'(z).  R is never materialised.
 template <bool TANH>
-struct AtRFusedSrc {
-  const float* Sh; const float* zq; const float* tq; const float* x; const float* dWl;  // dWl: LDS [D][128]
-  int T, D, H; int64_t rend; int n0;
+struct AtRFusedSrc {  // h side: R = (phi(z) - tgt) phi'(z) formed in the B loader (z includes X dWx)
+  const float* Sh; const float* zq; const float* tq;
+  int T, H; int64_t rend;
   static constexpr bool A_ROW_MAJOR = false;
   __device__ float4 a4(int64_t m, int64_t row) const {
     if (row >= rend || m >= H) return make_float4(0.f, 0.f, 0.f, 0.f);
@@ -395,17 +395,8 @@ struct AtRFusedSrc {
   __device__ float4 b4(int64_t row, int64_t j) const {
     if (row >= rend || j >= H) return make_float4(0.f, 0.f, 0.f, 0.f);
     const int64_t e = row * H + j;
-    float4 z4 = *reinterpret_cast<const float4*>(zq + e);
+    const float4 z4 = *reinterpret_cast<const float4*>(zq + e);
     const float4 t4 = *reinterpret_cast<const float4*>(tq + e);
-    const float* wl = dWl + (j - n0);
-#pragma unroll
-    for (int d = 0; d < kFastD; ++d) {
-      if (d < D) {
-        const float xd = x[row * D + d];
-        const float4 w = *reinterpret_cast<const float4*>(wl + d * 128);
-        z4.x += xd * w.x; z4.y += xd * w.y; z4.z += xd * w.z; z4.w += xd * w.w;
-      }
-    }
     float zz[4] = {z4.x, z4.y, z4.z, z4.w}, tt[4] = {t4.x, t4.y, t4.z, t4.w}, r[4];
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
@@ -429,7 +420,7 @@ __device__ __forceinline__ void atr_fused_body(const Geom& g, const float* x, co
                                                const float* tgt, const float* dW, float* slab, int nsplit,
                                                float* smem) {
   constexpr int BM = 128, BN = 128, WM = 64, WN = 64, KC = 32;
-  using S = Tile<BM, BN, WM, WN, KC>;
+  using S = Tile<BM, BN, WM, WN, KC, false>;
   const int nm = (g.H + BM - 1) / BM, nn = (g.H + BN - 1) / BN;
   int lid = xcd_swizzle(blockIdx.x, gridDim.x);
   const int mt = lid % nm; lid /= nm;
@@ -439,13 +430,7 @@ __device__ __forceinline__ void atr_fused_body(const Geom& g, const float* x, co
   const int64_t per = ((BT + nsplit - 1) / nsplit + KC - 1) / KC * KC;
   const int64_t r0 = sp * per, r1 = (r0 + per < BT) ? r0 + per : BT;
   const int m0 = mt * BM, n0 = nt * BN;
-  float* dWl = smem + S::LDS_FLOATS;   // after both engine stages
-  for (int i = threadIdx.x; i < g.D * BN; i += kThreads) {
-    const int d = i / BN, jj = n0 + i % BN;
-    dWl[i] = jj < g.H ? dW[((int64_t)q * g.D + d) * g.H + jj] : 0.f;
-  }
-  __syncthreads();
-  AtRFusedSrc<TANH> src{Sh, zc + (int64_t)q * n, tgt + (int64_t)q * n, x, dWl, g.T, g.D, g.H, r1, n0};
+  AtRFusedSrc<TANH> src{Sh, zc + (int64_t)q * n, tgt + (int64_t)q * n, g.T, g.H, r1};
   f32x16 acc[S::MT][S::NT];
   zero_acc(acc);
   Engine<BM, BN, WM, WN, KC, AtRFusedSrc<TANH>> eng;
@@ -467,7 +452,7 @@ __device__ __forceinline__ void atr_fused_body(const Geom& g, const float* x, co
     }
 }
 
-constexpr int ATR_FUSED_LDS = Tile<128, 128, 64, 64, 32>::LDS_FLOATS + kFastD * 128;
+constexpr int ATR_FUSED_LDS = Tile<128, 128, 64, 64, 32, false>::LDS_FLOATS;
 
 __global__ __launch_bounds__(kThreads) void k_atr_fused(Geom g, const float* x, const float* Sh, const float* zc,
                                                           const float* tgt, const float* dW, float* slab, int nsplit) {
@@ -684,67 +669,151 @@ struct RowCols {  // thread -> (row offset, float4 column) of a rows x (H/4) gri
   }
 };
 
-template <bool TANH, int SIDE>
-__device__ __forceinline__ void trial_fast_body(const Geom& g, int q, int pass, const float* zc, const float* tgt,
-                                                const float* Q, const float* x, const float* Wlds, float (&acc)[kSlots]) {
+// Fast-path input width: D is padded to DP in {4, 8, 12, 16} (the LDS weight rows d >= D
+// are zero, so the per-row x . W loops have compile-time trip counts).  XV: D == DP, the
+// x row is read with float4 loads; otherwise element loads masked by d < D.
+template <int DP, bool XV>
+__device__ __forceinline__ void load_xrow(const float* __restrict__ x, int64_t row, int D, float (&xr)[DP]) {
+  if (XV) {
+    const float4* p = reinterpret_cast<const float4*>(x + row * DP);
+#pragma unroll
+    for (int d4 = 0; d4 < DP / 4; ++d4) {
+      const float4 v = p[d4];
+      xr[4 * d4] = v.x; xr[4 * d4 + 1] = v.y; xr[4 * d4 + 2] = v.z; xr[4 * d4 + 3] = v.w;
+    }
+  } else {
+    const float* p = x + row * D;
+#pragma unroll
+    for (int d = 0; d < DP; ++d) xr[d] = d < D ? p[d] : 0.f;
+  }
+}
+
+// [DP][H] weight block of gate q into LDS, rows d >= D zeroed
+template <int DP>
+__device__ __forceinline__ void stage_wlds(const Geom& g, const float* __restrict__ src, float* wl) {
+  const int nW = g.D * g.H;
+  for (int i = threadIdx.x; i < DP * g.H; i += kThreads) wl[i] = i < nW ? src[i] : 0.f;
+  __syncthreads();
+}
+
+// dz = x_row . W[:, j..j+3] with W in LDS as [DP][H/4] float4
+template <int DP>
+__device__ __forceinline__ float4 xw_row(const float (&xr)[DP], const float4* __restrict__ wl4, int H4, int c4) {
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+  for (int d = 0; d < DP; ++d) {
+    const float4 wv = wl4[d * H4 + c4];
+    acc.x += xr[d] * wv.x; acc.y += xr[d] * wv.y; acc.z += xr[d] * wv.z; acc.w += xr[d] * wv.w;
+  }
+  return acc;
+}
+
+// Trial pass of the fast path over rows x float4 columns, two rows per thread per
+// iteration (all loads issued before any use; restrict pointers so they are not serialised
+// behind stores).  Side 0 forms the trial direction q = x_row . G_x[:, j] on the fly
+// (Wlds = G_x of this gate in LDS); side 1 reads Q.
+constexpr int kRPI = 2;
+
+template <bool TANH, int SIDE, int DP, bool XV>
+__device__ __forceinline__ void trial_fast_body(const Geom& g, int q, int pass, const float* __restrict__ zc,
+                                                const float* __restrict__ tgt, const float* __restrict__ Q,
+                                                const float* __restrict__ x, const float* Wlds, float (&acc)[kSlots]) {
   const int64_t BT = g.BT(), n = BT * g.H;
-  const float* zq = zc + (int64_t)q * n;
-  const float* tq = tgt + (int64_t)q * n;
-  const float* Qq = Q ? Q + (int64_t)q * n : nullptr;
+  const float* __restrict__ zq = zc + (int64_t)q * n;
+  const float* __restrict__ tq = tgt + (int64_t)q * n;
+  const float* __restrict__ Qq = Q ? Q + (int64_t)q * n : nullptr;
+  const float4* __restrict__ wl4 = reinterpret_cast<const float4*>(Wlds);
   RowCols rc(g.H);
   if (rc.rr >= rc.rpb) return;
-  const int j = 4 * rc.c4;          // fast path: H/4 <= 256, one float4 column per thread
-  for (int64_t row = (int64_t)blockIdx.x * rc.rpb + rc.rr; row < BT; row += (int64_t)gridDim.x * rc.rpb) {
-    const int64_t e = row * g.H + j;
-    float4 z4 = *reinterpret_cast<const float4*>(zq + e);
-    const float4 t4 = *reinterpret_cast<const float4*>(tq + e);
-    float4 w4 = make_float4(0.f, 0.f, 0.f, 0.f);
-    const float* xr = x + row * g.D;
-#pragma unroll 4
-    for (int d = 0; d < g.D; ++d) {
-      const float xd = xr[d];
-      const float4 wv = *reinterpret_cast<const float4*>(Wlds + d * g.H + j);
-      w4.x += xd * wv.x; w4.y += xd * wv.y; w4.z += xd * wv.z; w4.w += xd * wv.w;
+  const int j = 4 * rc.c4, H4 = g.H / 4;   // fast path: H/4 <= 256, one float4 column per thread
+  const int64_t stride = (int64_t)gridDim.x * rc.rpb;
+  for (int64_t row0 = (int64_t)blockIdx.x * rc.rpb + rc.rr; row0 < BT; row0 += kRPI * stride) {
+    float4 z4[kRPI], t4[kRPI], q4[kRPI];
+    float xr[kRPI][DP];
+#pragma unroll
+    for (int r = 0; r < kRPI; ++r) {
+      const int64_t row = row0 + r * stride;
+      if (row < BT) {
+        z4[r] = *reinterpret_cast<const float4*>(zq + row * g.H + j);
+        t4[r] = *reinterpret_cast<const float4*>(tq + row * g.H + j);
+        if (SIDE == 0) load_xrow<DP, XV>(x, row, g.D, xr[r]);
+        else q4[r] = *reinterpret_cast<const float4*>(Qq + row * g.H + j);
+      }
     }
-    float4 q4;
-    if (SIDE == 0) {
-      q4 = w4;
-    } else {
-      z4.x = z4.x + w4.x; z4.y = z4.y + w4.y; z4.z = z4.z + w4.z; z4.w = z4.w + w4.w;
-      q4 = *reinterpret_cast<const float4*>(Qq + e);
-    }
+#pragma unroll
+    for (int r = 0; r < kRPI; ++r) {
+      if (row0 + r * stride >= BT) break;
+      if (SIDE == 0) q4[r] = xw_row<DP>(xr[r], wl4, H4, rc.c4);
 #pragma unroll 1
-    for (int u = 0; u < 4; ++u) {
-      const float zu = u == 0 ? z4.x : (u == 1 ? z4.y : (u == 2 ? z4.z : z4.w));
-      const float tu = u == 0 ? t4.x : (u == 1 ? t4.y : (u == 2 ? t4.z : t4.w));
-      const float qu = u == 0 ? q4.x : (u == 1 ? q4.y : (u == 2 ? q4.z : q4.w));
-      trial_accumulate<TANH>(zu, tu, qu, pass, acc);
+      for (int u = 0; u < 4; ++u) {
+        const float zu = u == 0 ? z4[r].x : (u == 1 ? z4[r].y : (u == 2 ? z4[r].z : z4[r].w));
+        const float tu = u == 0 ? t4[r].x : (u == 1 ? t4[r].y : (u == 2 ? t4[r].z : t4[r].w));
+        const float qu = u == 0 ? q4[r].x : (u == 1 ? q4[r].y : (u == 2 ? q4[r].z : q4[r].w));
+        trial_accumulate<TANH>(zu, tu, qu, pass, acc);
+      }
     }
   }
 }
 
-// Wsrc: side 0 -> G_x [4][D][H]; side 1 -> dWx [4][D][H]
-template <int SIDE>
+// Wsrc: side 0 -> G_x [4][D][H]; side 1 -> unused (Q holds the h-side direction)
+template <int SIDE, int DP, bool XV>
 __global__ __launch_bounds__(kThreads) void k_trial_fast(Geom g, int pass, const float* zc, const float* tgt,
                                                            const float* Q, const float* x, const float* Wsrc,
                                                            const int* found, double* part, int nblk) {
-  extern __shared__ float wlds[];  // [D][H]
+  extern __shared__ float wlds[];  // [DP][H] (side 0 only)
   const int q = blockIdx.y;
   if (found[q]) return;
-  const int nW = g.D * g.H;
-  for (int i = threadIdx.x; i < nW; i += kThreads) wlds[i] = Wsrc[(int64_t)q * nW + i];
-  __syncthreads();
+  if (SIDE == 0) stage_wlds<DP>(g, Wsrc + (int64_t)q * g.D * g.H, wlds);
   float acc[kSlots];
 #pragma unroll
   for (int k = 0; k < kSlots; ++k) acc[k] = 0.f;
-  if (q == 2) trial_fast_body<true, SIDE>(g, q, pass, zc, tgt, Q, x, wlds, acc);
-  else trial_fast_body<false, SIDE>(g, q, pass, zc, tgt, Q, x, wlds, acc);
+  if (q == 2) trial_fast_body<true, SIDE, DP, XV>(g, q, pass, zc, tgt, Q, x, wlds, acc);
+  else trial_fast_body<false, SIDE, DP, XV>(g, q, pass, zc, tgt, Q, x, wlds, acc);
   trial_block_store(acc, part, q, nblk);
+}
+
+// After the x stage: zc += X dWx, so the h stage sees z = X Wx_new + Hprev Wh
+// (admm.py:298-300: the h-side search uses the already-updated x2q).
+template <int DP, bool XV>
+__global__ __launch_bounds__(kThreads) void k_apply_dwx(Geom g, const float* __restrict__ x,
+                                                          const float* __restrict__ dW, float* __restrict__ zc) {
+  extern __shared__ float wl[];  // [DP][H] of gate q
+  const int q = blockIdx.y;
+  stage_wlds<DP>(g, dW + (int64_t)q * g.D * g.H, wl);
+  const float4* __restrict__ wl4 = reinterpret_cast<const float4*>(wl);
+  const int64_t BT = g.BT();
+  float* __restrict__ zq = zc + (int64_t)q * BT * g.H;
+  RowCols rc(g.H);
+  if (rc.rr >= rc.rpb) return;
+  const int j = 4 * rc.c4, H4 = g.H / 4;
+  const int64_t stride = (int64_t)gridDim.x * rc.rpb;
+  for (int64_t row0 = (int64_t)blockIdx.x * rc.rpb + rc.rr; row0 < BT; row0 += kRPI * stride) {
+    float4 z4[kRPI];
+    float xr[kRPI][DP];
+#pragma unroll
+    for (int r = 0; r < kRPI; ++r) {
+      const int64_t row = row0 + r * stride;
+      if (row < BT) {
+        z4[r] = *reinterpret_cast<const float4*>(zq + row * g.H + j);
+        load_xrow<DP, XV>(x, row, g.D, xr[r]);
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < kRPI; ++r) {
+      const int64_t row = row0 + r * stride;
+      if (row >= BT) break;
+      const float4 dz = xw_row<DP>(xr[r], wl4, H4, rc.c4);
+      float4 zn;
+      zn.x = z4[r].x + dz.x; zn.y = z4[r].y + dz.y; zn.z = z4[r].z + dz.z; zn.w = z4[r].w + dz.w;
+      *reinterpret_cast<float4*>(zq + row * g.H + j) = zn;
+    }
+  }
 }
 
 // x-stage residual fused with G_x = X^T R (admm.py:302-312, x side): per element
 // tgt = lam/rho + S (stored for the trials and the h stage), R = (phi(z) - tgt) phi'(z),
 // and per block the partial sums X^T R into a [D][H] slab (R never reaches HBM).
+template <int DP, bool XV>
 __global__ __launch_bounds__(kThreads) void k_resid_gx(Geom g, Hyper hp, const float* x, Planes6 S, Planes6 L,
                                                          const float* zc, float* tgt, float* slab) {
   extern __shared__ float gl[];  // [D][H] block accumulator
@@ -758,18 +827,17 @@ __global__ __launch_bounds__(kThreads) void k_resid_gx(Geom g, Hyper hp, const f
   const float* Lq = L.p[q];
   RowCols rc(g.H);                 // fast path: H/4 <= 256, one float4 column per thread
   const int j = 4 * rc.c4;
-  float acc[kFastD][4];
+  float acc[DP][4];
 #pragma unroll
-  for (int d = 0; d < kFastD; ++d) acc[d][0] = acc[d][1] = acc[d][2] = acc[d][3] = 0.f;
+  for (int d = 0; d < DP; ++d) acc[d][0] = acc[d][1] = acc[d][2] = acc[d][3] = 0.f;
   const int64_t per_blk = (BT + gridDim.x - 1) / gridDim.x;
   const int64_t r0 = (int64_t)blockIdx.x * per_blk, r1 = r0 + per_blk < BT ? r0 + per_blk : BT;
   if (rc.rr < rc.rpb) {
     for (int64_t row = r0 + rc.rr; row < r1; row += rc.rpb) {
       const int64_t b = row / g.T;
       const int64_t so = (row + b + 1) * g.H;  // (b*(T+1) + t) * H with t = row - b*T + 1
-      float xr[kFastD];
-#pragma unroll
-      for (int d = 0; d < kFastD; ++d) xr[d] = d < g.D ? x[row * g.D + d] : 0.f;
+      float xr[DP];
+      load_xrow<DP, XV>(x, row, g.D, xr);
       const float4 z4 = *reinterpret_cast<const float4*>(zq + row * g.H + j);
       const float4 l4 = *reinterpret_cast<const float4*>(Lq + so + j);
       const float4 s4 = *reinterpret_cast<const float4*>(Sq + so + j);
@@ -790,7 +858,7 @@ __global__ __launch_bounds__(kThreads) void k_resid_gx(Geom g, Hyper hp, const f
         }
         const float R = (phi - tt[u]) * dphi;
 #pragma unroll
-        for (int d = 0; d < kFastD; ++d) acc[d][u] += xr[d] * R;
+        for (int d = 0; d < DP; ++d) acc[d][u] += xr[d] * R;
       }
     }
   }
@@ -800,7 +868,7 @@ __global__ __launch_bounds__(kThreads) void k_resid_gx(Geom g, Hyper hp, const f
   for (int grp = 0; grp < rc.rpb; ++grp) {
     if (rc.rr == grp) {
 #pragma unroll
-      for (int d = 0; d < kFastD; ++d) {
+      for (int d = 0; d < DP; ++d) {
         if (d < g.D) {
           float* dst = gl + d * g.H + j;
           dst[0] += acc[d][0]; dst[1] += acc[d][1]; dst[2] += acc[d][2]; dst[3] += acc[d][3];
@@ -1266,7 +1334,7 @@ void launch_trial_reduce(const Geom& g, int pass, const double* part, int nblk, 
 }
 
 bool fast_path(const Geom& g) {
-  return g.D <= kFastD && g.H % 4 == 0 && g.H / 4 <= kThreads && (int64_t)g.D * g.H * 4 <= 64 * 1024;
+  return g.D <= kFastD && g.H % 4 == 0 && g.H / 4 <= kThreads && (int64_t)kFastD * g.H * 4 <= 64 * 1024;
 }
 
 int resid_gx_blocks(const Geom& g) {
@@ -1274,10 +1342,28 @@ int resid_gx_blocks(const Geom& g) {
   return nb > 256 ? 256 : (nb < 1 ? 1 : nb);
 }
 
+// Calls f(integral_constant<DP>, integral_constant<XV>) for the padded input width of g.
+template <class F>
+void with_dp(const Geom& g, F&& f) {
+  using std::integral_constant;
+  const bool xv = (g.D % 4) == 0;
+  switch ((g.D + 3) / 4) {
+    case 1: xv ? f(integral_constant<int, 4>{}, std::true_type{}) : f(integral_constant<int, 4>{}, std::false_type{}); break;
+    case 2: xv ? f(integral_constant<int, 8>{}, std::true_type{}) : f(integral_constant<int, 8>{}, std::false_type{}); break;
+    case 3: xv ? f(integral_constant<int, 12>{}, std::true_type{}) : f(integral_constant<int, 12>{}, std::false_type{}); break;
+    default: xv ? f(integral_constant<int, 16>{}, std::true_type{}) : f(integral_constant<int, 16>{}, std::false_type{}); break;
+  }
+}
+
+size_t fast_lds(const Geom& g) { return (size_t)((g.D + 3) / 4) * 4 * g.H * sizeof(float); }
+
 void launch_resid_gx(const Geom& g, const Hyper& hp, const float* x, const Planes6& S, const Planes6& L,
                      const float* zc, float* tgt, float* slab, int nblk, hipStream_t s) {
   dim3 grid(nblk, 4);
-  k_resid_gx<<<grid, kThreads, (size_t)g.D * g.H * sizeof(float), s>>>(g, hp, x, S, L, zc, tgt, slab);
+  with_dp(g, [&](auto dp, auto xv) {
+    k_resid_gx<decltype(dp)::value, decltype(xv)::value>
+        <<<grid, kThreads, (size_t)g.D * g.H * sizeof(float), s>>>(g, hp, x, S, L, zc, tgt, slab);
+  });
 }
 
 void launch_atr_fused(const Geom& g, const Hyper& hp, const float* x, const float* Sh, const float* zc,
@@ -1287,12 +1373,31 @@ void launch_atr_fused(const Geom& g, const Hyper& hp, const float* x, const floa
   k_atr_fused<<<grid, kThreads, 0, s>>>(g, x, Sh, zc, tgt, dW, slab, nsplit);
 }
 
+int stream_blocks(const Geom& g) {   // streaming passes: ~2 rows in flight per thread
+  const int hchunk = g.H / 4 < kThreads ? g.H / 4 : kThreads;
+  const int rpb = kThreads / (hchunk > 0 ? hchunk : 1);
+  int nb = cdiv64(g.BT(), (int64_t)rpb * kRPI * 4);
+  return nb > 512 ? 512 : (nb < 1 ? 1 : nb);
+}
+
+void launch_apply_dwx(const Geom& g, const float* x, const float* dW, float* zc, hipStream_t s) {
+  dim3 grid(stream_blocks(g), 4);
+  with_dp(g, [&](auto dp, auto xv) {
+    k_apply_dwx<decltype(dp)::value, decltype(xv)::value><<<grid, kThreads, fast_lds(g), s>>>(g, x, dW, zc);
+  });
+}
+
 void launch_trial_fast(const Geom& g, int side, int pass, const float* zc, const float* tgt, const float* Q,
                        const float* x, const float* Wsrc, const int* found, double* part, int nblk, hipStream_t s) {
   dim3 grid(nblk, 4);
-  const size_t lds = (size_t)g.D * g.H * sizeof(float);
-  if (side == 0) k_trial_fast<0><<<grid, kThreads, lds, s>>>(g, pass, zc, tgt, Q, x, Wsrc, found, part, nblk);
-  else k_trial_fast<1><<<grid, kThreads, lds, s>>>(g, pass, zc, tgt, Q, x, Wsrc, found, part, nblk);
+  if (side == 1) {  // no x . W product on this side: one instantiation
+    k_trial_fast<1, 4, false><<<grid, kThreads, 0, s>>>(g, pass, zc, tgt, Q, x, Wsrc, found, part, nblk);
+    return;
+  }
+  with_dp(g, [&](auto dp, auto xv) {
+    k_trial_fast<0, decltype(dp)::value, decltype(xv)::value>
+        <<<grid, kThreads, fast_lds(g), s>>>(g, pass, zc, tgt, Q, x, Wsrc, found, part, nblk);
+  });
 }
 
 void launch_select(const Geom& g, const Hyper& hp, const SelectArgs& a, hipStream_t s) {

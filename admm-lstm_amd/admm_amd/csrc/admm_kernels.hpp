@@ -121,7 +121,10 @@ void launch_resid_gx(const Geom& g, const Hyper& hp, const float* x, const Plane
 // trial pass without a materialised Q (side 0: q = x.G_x) or z (side 1: z = zc + x.dWx)
 void launch_trial_fast(const Geom& g, int side, int pass, const float* zc, const float* tgt, const float* Q,
                        const float* x, const float* Wsrc, const int* found, double* part, int nblk, hipStream_t s);
-// h stage A^T R with R computed on the fly from zc, tgt, x, dWx (side 1, fast path)
+int stream_blocks(const Geom& g);   // grid (per gate) of the fast streaming passes
+// after the x stage (fast path): zc += X dWx
+void launch_apply_dwx(const Geom& g, const float* x, const float* dW, float* zc, hipStream_t s);
+// h stage A^T R with R computed on the fly from zc (already updated) and tgt (side 1, fast path)
 void launch_atr_fused(const Geom& g, const Hyper& hp, const float* x, const float* Sh, const float* zc,
                       const float* tgt, const float* dW, float* slab, int nsplit, hipStream_t s);
 // decide the first passing k in this pass's window; on success update the weights

@@ -1,0 +1,81 @@
+// Isolated timing of the library's kernels (admm_kernels.hip launchers) on random C3 data.
+// build: see tools/kbench.sh ; run on the GPU box.
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include <cstdlib>
+#include <functional>
+#include <random>
+#include <vector>
+#include "../admm-lstm_amd/admm_amd/csrc/admm_kernels.hpp"
+
+using namespace admm;
+
+static float* dev_random(size_t n, float lo, float hi, unsigned seed) {
+  std::vector<float> h(n);
+  std::mt19937 rng(seed);
+  std::uniform_real_distribution<float> u(lo, hi);
+  for (auto& v : h) v = u(rng);
+  float* d;
+  (void)hipMalloc(&d, n * 4);
+  (void)hipMemcpy(d, h.data(), n * 4, hipMemcpyHostToDevice);
+  return d;
+}
+
+static void timeit(const char* name, double bytes, double flops, const std::function<void()>& f) {
+  hipEvent_t a, b;
+  (void)hipEventCreate(&a); (void)hipEventCreate(&b);
+  for (int i = 0; i < 3; ++i) f();
+  (void)hipDeviceSynchronize();
+  const int R = 10;
+  (void)hipEventRecord(a);
+  for (int i = 0; i < R; ++i) f();
+  (void)hipEventRecord(b);
+  (void)hipEventSynchronize(b);
+  float ms; (void)hipEventElapsedTime(&ms, a, b);
+  ms /= R;
+  printf("%-22s %8.3f ms  %7.0f GB/s  %6.1f TF/s\n", name, ms, bytes / ms / 1e6, flops / ms / 1e9);
+}
+
+int main(int argc, char** argv) {
+  Geom g{8192, 8192, 32, 16, 256, 1};
+  if (argc > 1) g.B = g.Bg = atoll(argv[1]);
+  const int64_t BT = g.BT(), n = BT * g.H, P = g.B * (int64_t)g.TP() * g.H;
+  Hyper hp{};
+  for (int i = 0; i < 7; ++i) hp.rho[i] = 1.f;
+  hp.rho[4] = 0.008f; hp.rho[5] = 0.00045f; hp.rho[6] = 5.62e-5f;
+  float* x = dev_random(BT * g.D, 0, 1, 1);
+  float* zc = dev_random(4 * n, -2, 2, 2);
+  float* tgt = dev_random(4 * n, 0, 1, 3);
+  float* Q = dev_random(4 * n, -1e-4f, 1e-4f, 4);
+  float* R = dev_random(4 * n, -1e-3f, 1e-3f, 5);
+  Planes6 S, L;
+  for (int q = 0; q < 6; ++q) { S.p[q] = dev_random(P, 0, 1, 10 + q); L.p[q] = dev_random(P, -1e-3f, 1e-3f, 20 + q); }
+  float* W[8];
+  for (int i = 0; i < 8; ++i) W[i] = dev_random(i < 4 ? g.D * g.H : g.H * g.H, -0.1f, 0.1f, 30 + i);
+  Weights w;
+  for (int q = 0; q < 4; ++q) { w.wx[q] = W[q]; w.wh[q] = W[4 + q]; }
+  float* G = dev_random(4 * g.H * g.H, -1e-3f, 1e-3f, 40);
+  float* dW = dev_random(4 * g.D * g.H, -1e-4f, 1e-4f, 41);
+  float* slab; (void)hipMalloc(&slab, (size_t)256 * 4 * g.H * g.H * 4);
+  double* part; (void)hipMalloc(&part, (size_t)4 * kTrialSlots * 4096 * 8);
+  int* found; (void)hipMalloc(&found, 16); (void)hipMemset(found, 0, 16);
+  hipStream_t s = 0;
+  const double f4 = 4.0;
+  const int nb = stream_blocks(g);
+  timeit("apply_dwx", 2 * f4 * 4 * n + f4 * BT * g.D, 0, [&] { launch_apply_dwx(g, x, dW, zc, s); });
+  timeit("trial_fast side0", f4 * 2 * 4 * n, 0, [&] { launch_trial_fast(g, 0, 0, zc, tgt, nullptr, x, G, found, part, nb, s); });
+  timeit("trial_fast side1", f4 * 3 * 4 * n, 0, [&] { launch_trial_fast(g, 1, 0, zc, tgt, Q, x, dW, found, part, nb, s); });
+  timeit("trial generic", f4 * 3 * 4 * n, 0, [&] { launch_trial(g, 0, zc, tgt, Q, found, part, trial_blocks(g), s); });
+  timeit("resid_gx", f4 * 4 * 4 * n, 0, [&] { launch_resid_gx(g, hp, x, S, L, zc, tgt, slab, resid_gx_blocks(g), s); });
+  const int ns = atr_splits(g, 1);
+  timeit("atr_fused", f4 * (2 * 4 * n + BT * g.H), 2.0 * BT * g.H * 4 * g.H,
+         [&] { launch_atr_fused(g, hp, x, S.p[5], zc, tgt, dW, slab, ns, s); });
+  timeit("atr (R materialised)", f4 * (4 * n + BT * g.H), 2.0 * BT * g.H * 4 * g.H,
+         [&] { launch_atr(g, 1, x, S.p[5], R, slab, ns, s); });
+  timeit("qgemm side1", f4 * (4 * n + BT * g.H), 2.0 * BT * g.H * 4 * g.H, [&] { launch_qgemm(g, 1, x, S.p[5], G, Q, s); });
+  SweepT sw{x, S, L, zc};
+  timeit("sweep_t (t=5)", f4 * g.B * (g.D + 27.0 * g.H), 2.0 * g.B * (g.D + g.H) * 4 * g.H,
+         [&] { launch_sweep_t(g, 5, w, hp, sw, s); });
+  timeit("zgemm", f4 * (4 * n + BT * (g.D + g.H)), 2.0 * BT * (g.D + g.H) * 4 * g.H, [&] { launch_zgemm(g, w, x, S.p[5], zc, s); });
+  return 0;
+}

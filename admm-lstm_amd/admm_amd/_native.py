@@ -55,7 +55,8 @@ class AdmmBuffers(Structure):
 
 class AdmmStats(Structure):
     _fields_ = [('steps', c_int32), ('k', c_int32 * 8), ('passes', c_int32 * 2), ('f_w', c_double * 8),
-                ('grad_sq', c_double * 8), ('theta_h', c_float), ('unresolved', c_int32), ('nonfinite', c_int32)]
+                ('grad_sq', c_double * 8), ('theta_h', c_float), ('unresolved', c_int32), ('nonfinite', c_int32),
+                ('direct_frac', c_double * 8)]
 
 
 # name -> (restype, argtypes)

@@ -9,6 +9,7 @@
 //    LDS staging, used by the time-step GEMM, the Q = A*G GEMM and the A^T*R reduction.
 #pragma once
 #include <hip/hip_runtime.h>
+#include <type_traits>
 #include <stdint.h>
 
 namespace admm {
@@ -180,10 +181,26 @@ __device__ __forceinline__ int xcd_swizzle(int bid, int nb) {
 
 __device__ __forceinline__ int acc_row(int r, int lane) { return (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5); }
 
+// Two-phase B operand: a source with a BRaw type splits b4 into braw (the global loads,
+// issued ahead of the MFMAs) and bfin (the element-wise transform, run at LDS-store time,
+// after this chunk's MFMAs have been issued, so its VALU work overlaps the matrix pipe).
+template <class P, class = void>
+struct BRawOf {
+  using type = float4;
+  static constexpr bool two_phase = false;
+};
+template <class P>
+struct BRawOf<P, std::void_t<typename P::BRaw>> {
+  using type = typename P::BRaw;
+  static constexpr bool two_phase = true;
+};
+
 template <int BM, int BN, int WM, int WN, int KC, class P>
 struct Engine {
   using S = Tile<BM, BN, WM, WN, KC, P::A_ROW_MAJOR>;
-  float4 ra[S::A_PER], rb[S::B_PER];
+  using BR = BRawOf<P>;
+  float4 ra[S::A_PER];
+  typename BR::type rb[S::B_PER];
 
   __device__ __forceinline__ void load(const P& p, int64_t m0, int64_t n0, int64_t kb) {
     const int tid = threadIdx.x;
@@ -198,11 +215,14 @@ struct Engine {
 #pragma unroll
     for (int i = 0; i < S::B_PER; ++i) {
       const int f = tid + i * kThreads;
-      if (f < S::B4) rb[i] = p.b4(kb + f / (BN / 4), n0 + 4 * (f % (BN / 4)));
+      if (f < S::B4) {
+        if constexpr (BR::two_phase) rb[i] = p.braw(kb + f / (BN / 4), n0 + 4 * (f % (BN / 4)));
+        else rb[i] = p.b4(kb + f / (BN / 4), n0 + 4 * (f % (BN / 4)));
+      }
     }
   }
 
-  __device__ __forceinline__ void store(float* As, float* Bs) const {
+  __device__ __forceinline__ void store(const P& p, float* As, float* Bs) const {
     const int tid = threadIdx.x;
 #pragma unroll
     for (int i = 0; i < S::A_PER; ++i) {
@@ -217,7 +237,12 @@ struct Engine {
 #pragma unroll
     for (int i = 0; i < S::B_PER; ++i) {
       const int f = tid + i * kThreads;
-      if (f < S::B4) *reinterpret_cast<float4*>(&Bs[(f / (BN / 4)) * S::BS + 4 * (f % (BN / 4))]) = rb[i];
+      if (f < S::B4) {
+        float4 v;
+        if constexpr (BR::two_phase) v = p.bfin(rb[i]);
+        else v = rb[i];
+        *reinterpret_cast<float4*>(&Bs[(f / (BN / 4)) * S::BS + 4 * (f % (BN / 4))]) = v;
+      }
     }
   }
 
@@ -273,7 +298,7 @@ struct Engine {
                                       f32x16 (&acc)[S::MT][S::NT], float* smem) {
     if (k0 >= k1) return;
     load(p, m0, n0, k0);
-    store(smem, smem + S::A_FLOATS);
+    store(p, smem, smem + S::A_FLOATS);
     __syncthreads();
     int stage = 0;
     for (int64_t kb = k0; kb < k1; kb += KC) {
@@ -283,7 +308,7 @@ struct Engine {
       compute(cur, cur + S::A_FLOATS, acc);
       if (more) {
         float* nxt = smem + (stage ^ 1) * S::STAGE_FLOATS;
-        store(nxt, nxt + S::A_FLOATS);
+        store(p, nxt, nxt + S::A_FLOATS);
       }
       __syncthreads();
       stage ^= 1;

@@ -269,6 +269,8 @@ int check_dims(const AdmmDims* d) {
                 d->seq_len, d->input_size, d->hidden_size, d->output_size);
   if (d->global_batch < d->batch) return fail(ADMM_EINVAL, "global_batch < batch");
   if (d->output_size > 8) return fail(ADMM_EINVAL, "output_size %d > 8 is not supported", d->output_size);
+  if (d->batch * (int64_t)d->seq_len >= (1ll << 31))
+    return fail(ADMM_EINVAL, "batch*seq_len = %lld rows per device exceeds 2^31-1", (long long)(d->batch * (int64_t)d->seq_len));
   return ADMM_OK;
 }
 
@@ -304,6 +306,7 @@ int admm_create(const AdmmDims* dims, const AdmmParams* params, int device, Admm
   g.D = dims->input_size;
   g.H = dims->hidden_size;
   g.O = dims->output_size;
+  g.set_T();
   Hyper& h = c->hp;
   for (int i = 0; i < 7; ++i) h.rho[i] = params->rho[i];
   for (int q = 0; q < 4; ++q) {
@@ -508,6 +511,7 @@ int admm_get_stats(AdmmCtx* c, AdmmStats* out) {
     out->k[i] = d.k[i];
     out->f_w[i] = d.f_w[i];
     out->grad_sq[i] = d.grad_sq[i];
+    out->direct_frac[i] = d.direct_frac[i];
   }
   out->passes[0] = d.passes[0];
   out->passes[1] = d.passes[1];
@@ -550,6 +554,7 @@ int admm_forward(const float* x, int64_t batch, int32_t seq_len, int32_t input_s
   if (!gates_out && (!h_scratch || !c_scratch)) return fail(ADMM_EINVAL, "admm_forward: need gates_out or scratch");
   hipStream_t s = (hipStream_t)stream;
   Geom g{batch, batch, seq_len, input_size, hidden_size, output_size};
+  g.set_T();
   Weights w;
   for (int q = 0; q < 4; ++q) {
     if (!wx[q] || !wh[q]) return fail(ADMM_EINVAL, "admm_forward: NULL weight");

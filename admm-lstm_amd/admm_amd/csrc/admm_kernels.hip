@@ -196,20 +196,20 @@ __global__ __launch_bounds__(kThreads) void k_rowdot(int64_t B, int H, int O, co
 
 template <bool VEC>
 struct AllRowSrc {  // z cache recompute: A = [X | Hprev] over all rows (K = D+H), B = [Wx; Wh]
-  const float* x; const float* Sh; int64_t BT; int T, D, H; Weights w; int j0;
+  const float* x; const float* Sh; int64_t BT; DivU32 dT; int D, H; Weights w; int j0;
   static constexpr bool A_ROW_MAJOR = true;
   __device__ float4 a4(int64_t m, int64_t k) const {
     const int K = D + H;
     if (VEC) {
       if (m >= BT || k >= K) return make_float4(0.f, 0.f, 0.f, 0.f);
-      const float* src = k < D ? x + m * D + k : Sh + (m + m / T) * H + (k - D);
+      const float* src = k < D ? x + m * D + k : Sh + (m + dT.div((uint32_t)m)) * H + (k - D);
       return *reinterpret_cast<const float4*>(src);
     }
     float v[4];
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const int64_t kk = k + u;
-      v[u] = (m < BT && kk < K) ? (kk < D ? x[m * D + kk] : Sh[(m + m / T) * H + (kk - D)]) : 0.f;
+      v[u] = (m < BT && kk < K) ? (kk < D ? x[m * D + kk] : Sh[(m + dT.div((uint32_t)m)) * H + (kk - D)]) : 0.f;
     }
     return make_float4(v[0], v[1], v[2], v[3]);
   }
@@ -224,7 +224,7 @@ __device__ __forceinline__ void zgemm_body(const Geom& g, const Weights& w, cons
   const int64_t m0 = (int64_t)(lid / nj) * TS_BM;
   const int j0 = (lid % nj) * 32;
   const int64_t BT = g.BT();
-  AllRowSrc<VEC> src{x, Sh, BT, g.T, g.D, g.H, w, j0};
+  AllRowSrc<VEC> src{x, Sh, BT, g.dT, g.D, g.H, w, j0};
   f32x16 acc[1][4];
   zero_acc(acc);
   Engine<TS_BM, TS_BN, TS_WM, TS_WN, TS_KC, AllRowSrc<VEC>> eng;
@@ -274,7 +274,7 @@ __global__ __launch_bounds__(kThreads) void k_resid(Geom g, Hyper hp, ResidArgs 
   RowJ ix(g.H);
   if (ix.rr < ix.rpb) {
     for (int64_t row = (int64_t)blockIdx.x * ix.rpb + ix.rr; row < BT; row += (int64_t)gridDim.x * ix.rpb) {
-      const int64_t b = row / g.T;
+      const int64_t b = g.dT.div((uint32_t)row);
       const int t = (int)(row - b * g.T) + 1;
       const int64_t so = (b * g.TP() + t) * g.H;
       for (int j = ix.jj; j < g.H; j += ix.hchunk) {
@@ -307,13 +307,13 @@ __global__ __launch_bounds__(kThreads) void k_resid(Geom g, Hyper hp, ResidArgs 
 
 // G_q = A^T R_q split over rows.  Side 1 (A = Hprev, Kd = H): 128 x 128 tiles, 2x2 waves
 // of 64x64; side 0 (A = X, Kd = D small): 32 x 128 tiles.
-template <bool VEC>
+template <bool VEC, int SIDE>
 struct AtRSrc {  // A^T: A stored [row][m] (m contiguous); B = R[q] [row][j]
-  const float* x; const float* Sh; const float* Rq; int side; int T, D, H, Kd; int64_t rend;
+  const float* x; const float* Sh; const float* Rq; DivU32 dT; int D, H, Kd; int64_t rend;
   static constexpr bool A_ROW_MAJOR = false;
   __device__ float4 a4(int64_t m, int64_t row) const {
     if (row >= rend) return make_float4(0.f, 0.f, 0.f, 0.f);
-    const float* base = side == 0 ? x + row * D : Sh + (row + row / T) * H;
+    const float* base = SIDE == 0 ? x + row * D : Sh + (row + dT.div((uint32_t)row)) * H;
     if (VEC) {
       if (m >= Kd) return make_float4(0.f, 0.f, 0.f, 0.f);
       return *reinterpret_cast<const float4*>(base + m);
@@ -336,12 +336,12 @@ struct AtRSrc {  // A^T: A stored [row][m] (m contiguous); B = R[q] [row][j]
   }
 };
 
-template <int BM, int WM, bool VEC>
-__device__ __forceinline__ void atr_body(const Geom& g, int side, const float* x, const float* Sh, const float* R,
+template <int BM, int WM, bool VEC, int SIDE>
+__device__ __forceinline__ void atr_body(const Geom& g, const float* x, const float* Sh, const float* R,
                                          float* slab, int nsplit, float* smem) {
   constexpr int BN = 128, WN = (BM == 128) ? 64 : 32, KC = 32;
   using S = Tile<BM, BN, WM, WN, KC, false>;
-  const int Kd = side == 0 ? g.D : g.H;
+  const int Kd = SIDE == 0 ? g.D : g.H;
   const int nm = (Kd + BM - 1) / BM, nn = (g.H + BN - 1) / BN;
   int lid = xcd_swizzle(blockIdx.x, gridDim.x);
   const int mt = lid % nm; lid /= nm;
@@ -351,10 +351,10 @@ __device__ __forceinline__ void atr_body(const Geom& g, int side, const float* x
   const int64_t per = ((BT + nsplit - 1) / nsplit + KC - 1) / KC * KC;
   const int64_t r0 = sp * per, r1 = (r0 + per < BT) ? r0 + per : BT;
   const int m0 = mt * BM, n0 = nt * BN;
-  AtRSrc<VEC> src{x, Sh, R + (int64_t)q * BT * g.H, side, g.T, g.D, g.H, Kd, r1};
+  AtRSrc<VEC, SIDE> src{x, Sh, R + (int64_t)q * BT * g.H, g.dT, g.D, g.H, Kd, r1};
   f32x16 acc[S::MT][S::NT];
   zero_acc(acc);
-  Engine<BM, BN, WM, WN, KC, AtRSrc<VEC>> eng;
+  Engine<BM, BN, WM, WN, KC, AtRSrc<VEC, SIDE>> eng;
   if (r0 < r1) eng.run(src, m0, n0, r0, r1, acc, smem);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int wm0 = (wave / S::WAVES_N) * WM, wn0 = (wave % S::WAVES_N) * WN;
@@ -373,31 +373,37 @@ __device__ __forceinline__ void atr_body(const Geom& g, int side, const float* x
     }
 }
 
-template <int BM, int WM, bool VEC>
-__global__ __launch_bounds__(kThreads) void k_atr(Geom g, int side, const float* x, const float* Sh,
+template <int BM, int WM, bool VEC, int SIDE>
+__global__ __launch_bounds__(kThreads) void k_atr(Geom g, const float* x, const float* Sh,
                                                     const float* R, float* slab, int nsplit) {
   __shared__ float smem[Tile<BM, 128, WM, (BM == 128) ? 64 : 32, 32, false>::LDS_FLOATS];
-  atr_body<BM, WM, VEC>(g, side, x, Sh, R, slab, nsplit, smem);
+  atr_body<BM, WM, VEC, SIDE>(g, x, Sh, R, slab, nsplit, smem);
 }
 
 // h-stage A^T R with the residual formed in the B-operand loader (admm.py:302-312, h side):
-// z = zc + x_row . dWx (the x-side update, already applied to the weights), then
-// R = (phi(z) - tgt) phi'(z).  R is never materialised.
+// z (the cached pre-activation with X dWx already applied by k_apply_dwx) and the target
+// are loaded ahead of the MFMAs; R = (phi(z) - tgt) phi'(z) is formed at LDS-store time.
+// R is never materialised.
 template <bool TANH>
-struct AtRFusedSrc {  // h side: R = (phi(z) - tgt) phi'(z) formed in the B loader (z includes X dWx)
+struct AtRFusedSrc {
   const float* Sh; const float* zq; const float* tq;
-  int T, H; int64_t rend;
+  DivU32 dT; int H; int64_t rend;
   static constexpr bool A_ROW_MAJOR = false;
+  struct BRaw { float4 z, t; };
   __device__ float4 a4(int64_t m, int64_t row) const {
     if (row >= rend || m >= H) return make_float4(0.f, 0.f, 0.f, 0.f);
-    return *reinterpret_cast<const float4*>(Sh + (row + row / T) * H + m);
+    return *reinterpret_cast<const float4*>(Sh + (row + dT.div((uint32_t)row)) * H + m);
   }
-  __device__ float4 b4(int64_t row, int64_t j) const {
-    if (row >= rend || j >= H) return make_float4(0.f, 0.f, 0.f, 0.f);
+  __device__ BRaw braw(int64_t row, int64_t j) const {
+    // out of range: z = 0 with tgt = phi(0) (0.5 / 0, both exact) gives R = 0
+    const float t0 = TANH ? 0.f : 0.5f;
+    if (row >= rend || j >= H) return BRaw{make_float4(0.f, 0.f, 0.f, 0.f), make_float4(t0, t0, t0, t0)};
     const int64_t e = row * H + j;
-    const float4 z4 = *reinterpret_cast<const float4*>(zq + e);
-    const float4 t4 = *reinterpret_cast<const float4*>(tq + e);
-    float zz[4] = {z4.x, z4.y, z4.z, z4.w}, tt[4] = {t4.x, t4.y, t4.z, t4.w}, r[4];
+    return BRaw{*reinterpret_cast<const float4*>(zq + e), *reinterpret_cast<const float4*>(tq + e)};
+  }
+  __device__ float4 bfin(const BRaw& v) const {
+    const float zz[4] = {v.z.x, v.z.y, v.z.z, v.z.w}, tt[4] = {v.t.x, v.t.y, v.t.z, v.t.w};
+    float r[4];
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       float phi, dphi;
@@ -430,7 +436,7 @@ __device__ __forceinline__ void atr_fused_body(const Geom& g, const float* x, co
   const int64_t per = ((BT + nsplit - 1) / nsplit + KC - 1) / KC * KC;
   const int64_t r0 = sp * per, r1 = (r0 + per < BT) ? r0 + per : BT;
   const int m0 = mt * BM, n0 = nt * BN;
-  AtRFusedSrc<TANH> src{Sh, zc + (int64_t)q * n, tgt + (int64_t)q * n, g.T, g.H, r1};
+  AtRFusedSrc<TANH> src{Sh, zc + (int64_t)q * n, tgt + (int64_t)q * n, g.dT, g.H, r1};
   f32x16 acc[S::MT][S::NT];
   zero_acc(acc);
   Engine<BM, BN, WM, WN, KC, AtRFusedSrc<TANH>> eng;
@@ -473,13 +479,13 @@ __global__ __launch_bounds__(kThreads) void k_reduce_g(int Kd, int H, Hyper hp, 
   G[i] = (float)s * hp.rho[q];  // (sum_t A_t^T R_t) * rho (admm.py:312)
 }
 
-template <bool VEC>
+template <bool VEC, int SIDE>
 struct QSrc {  // A = X or Hprev rows (row-major, K = Kd); B = G_q [Kd][H]
-  const float* x; const float* Sh; const float* G; int64_t BT; int side, T, D, H, Kd, j0;
+  const float* x; const float* Sh; const float* G; int64_t BT; DivU32 dT; int D, H, Kd, j0;
   static constexpr bool A_ROW_MAJOR = true;
   __device__ float4 a4(int64_t row, int64_t k) const {
     if (row >= BT) return make_float4(0.f, 0.f, 0.f, 0.f);
-    const float* base = side == 0 ? x + row * D : Sh + (row + row / T) * H;
+    const float* base = SIDE == 0 ? x + row * D : Sh + (row + dT.div((uint32_t)row)) * H;
     if (VEC) {
       if (k >= Kd) return make_float4(0.f, 0.f, 0.f, 0.f);
       return *reinterpret_cast<const float4*>(base + k);
@@ -504,19 +510,19 @@ struct QSrc {  // A = X or Hprev rows (row-major, K = Kd); B = G_q [Kd][H]
 };
 
 // Q_q = A G_q: the trial direction, so that z(W + G/theta) = z(W) + Q / theta exactly.
-template <bool VEC>
-__device__ __forceinline__ void qgemm_body(const Geom& g, int side, const float* x, const float* Sh, const float* G,
+template <bool VEC, int SIDE>
+__device__ __forceinline__ void qgemm_body(const Geom& g, const float* x, const float* Sh, const float* G,
                                            float* Q, float* smem) {
-  const int Kd = side == 0 ? g.D : g.H;
+  const int Kd = SIDE == 0 ? g.D : g.H;
   const int nj = (g.H + 31) / 32;
   const int lid = xcd_swizzle(blockIdx.x, gridDim.x);
   const int64_t m0 = (int64_t)(lid / nj) * TS_BM;
   const int j0 = (lid % nj) * 32;
   const int64_t BT = g.BT();
-  QSrc<VEC> src{x, Sh, G, BT, side, g.T, g.D, g.H, Kd, j0};
+  QSrc<VEC, SIDE> src{x, Sh, G, BT, g.dT, g.D, g.H, Kd, j0};
   f32x16 acc[1][4];
   zero_acc(acc);
-  Engine<TS_BM, TS_BN, TS_WM, TS_WN, TS_KC, QSrc<VEC>> eng;
+  Engine<TS_BM, TS_BN, TS_WM, TS_WN, TS_KC, QSrc<VEC, SIDE>> eng;
   eng.run(src, m0, 0, 0, Kd, acc, smem);
   const int lane = threadIdx.x & 63, wm0 = (threadIdx.x >> 6) * TS_WM;
   const int j = j0 + (lane & 31);
@@ -530,11 +536,11 @@ __device__ __forceinline__ void qgemm_body(const Geom& g, int side, const float*
   }
 }
 
-template <bool VEC>
-__global__ __launch_bounds__(kThreads) void k_qgemm(Geom g, int side, const float* x, const float* Sh,
+template <bool VEC, int SIDE>
+__global__ __launch_bounds__(kThreads) void k_qgemm(Geom g, const float* x, const float* Sh,
                                                       const float* G, float* Q) {
   __shared__ float smem[TSTile::LDS_FLOATS];
-  qgemm_body<VEC>(g, side, x, Sh, G, Q, smem);
+  qgemm_body<VEC, SIDE>(g, x, Sh, G, Q, smem);
 }
 
 // Trial pass.  For the line search (admm.py:316-336) each gate needs, for k = 0, 1, ...,
@@ -834,7 +840,7 @@ __global__ __launch_bounds__(kThreads) void k_resid_gx(Geom g, Hyper hp, const f
   const int64_t r0 = (int64_t)blockIdx.x * per_blk, r1 = r0 + per_blk < BT ? r0 + per_blk : BT;
   if (rc.rr < rc.rpb) {
     for (int64_t row = r0 + rc.rr; row < r1; row += rc.rpb) {
-      const int64_t b = row / g.T;
+      const int64_t b = g.dT.div((uint32_t)row);
       const int64_t so = (row + b + 1) * g.H;  // (b*(T+1) + t) * H with t = row - b*T + 1
       float xr[DP];
       load_xrow<DP, XV>(x, row, g.D, xr);
@@ -981,6 +987,7 @@ __global__ __launch_bounds__(kThreads) void k_select(Geom g, Hyper hp, SelectArg
       a.stats->k[slot] = pick;
       a.stats->f_w[slot] = 0.5 * (double)rho * sm[kSlotFw];
       a.stats->grad_sq[slot] = gsq;
+      a.stats->direct_frac[slot] = sm[kSlotNne] / ((double)g.Bg * g.T * g.H);
       a.stats->passes[a.side] = a.pass + 1;
       a.found[q] = 1;
     }
@@ -1289,11 +1296,11 @@ void launch_atr(const Geom& g, int side, const float* x, const float* Sh, const 
   const int Kd = side == 0 ? g.D : g.H;
   dim3 grid(cdiv64(Kd, side == 1 ? 128 : 32) * cdiv64(g.H, 128) * 4 * nsplit);
   if (side == 1) {
-    if (vec_ok(g)) k_atr<128, 64, true><<<grid, kThreads, 0, s>>>(g, side, x, Sh, R, slab, nsplit);
-    else k_atr<128, 64, false><<<grid, kThreads, 0, s>>>(g, side, x, Sh, R, slab, nsplit);
+    if (vec_ok(g)) k_atr<128, 64, true, 1><<<grid, kThreads, 0, s>>>(g, x, Sh, R, slab, nsplit);
+    else k_atr<128, 64, false, 1><<<grid, kThreads, 0, s>>>(g, x, Sh, R, slab, nsplit);
   } else {
-    if (vec_ok(g)) k_atr<32, 32, true><<<grid, kThreads, 0, s>>>(g, side, x, Sh, R, slab, nsplit);
-    else k_atr<32, 32, false><<<grid, kThreads, 0, s>>>(g, side, x, Sh, R, slab, nsplit);
+    if (vec_ok(g)) k_atr<32, 32, true, 0><<<grid, kThreads, 0, s>>>(g, x, Sh, R, slab, nsplit);
+    else k_atr<32, 32, false, 0><<<grid, kThreads, 0, s>>>(g, x, Sh, R, slab, nsplit);
   }
 }
 
@@ -1307,8 +1314,13 @@ void launch_reduce_g(const Geom& g, int side, const Hyper& hp, const float* slab
 void launch_qgemm(const Geom& g, int side, const float* x, const float* Sh, const float* G, float* Q,
                   hipStream_t s) {
   dim3 grid(cdiv64(g.BT(), TS_BM) * cdiv64(g.H, 32));
-  if (vec_ok(g)) k_qgemm<true><<<grid, kThreads, 0, s>>>(g, side, x, Sh, G, Q);
-  else k_qgemm<false><<<grid, kThreads, 0, s>>>(g, side, x, Sh, G, Q);
+  if (side == 0) {
+    if (vec_ok(g)) k_qgemm<true, 0><<<grid, kThreads, 0, s>>>(g, x, Sh, G, Q);
+    else k_qgemm<false, 0><<<grid, kThreads, 0, s>>>(g, x, Sh, G, Q);
+  } else {
+    if (vec_ok(g)) k_qgemm<true, 1><<<grid, kThreads, 0, s>>>(g, x, Sh, G, Q);
+    else k_qgemm<false, 1><<<grid, kThreads, 0, s>>>(g, x, Sh, G, Q);
+  }
 }
 
 int trial_blocks(const Geom& g) {

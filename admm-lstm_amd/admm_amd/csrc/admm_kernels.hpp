@@ -16,12 +16,32 @@ constexpr int kFastD = 16;       // fused weight-stage path for input_size <= 16
 constexpr int kHTCand = 4;       // theta = 0.1, 0.2, 0.4, 0.8 (admm.py:447-480)
 constexpr int kHTSums = 1 + 3 * kHTCand;
 
+// n / d for 0 <= n < 2^31 by multiply-high (Granlund-Montgomery): no integer division in
+// the GEMM operand loaders.  make() runs on the host.
+struct DivU32 {
+  uint32_t m = 1;
+  int s = 0;
+  static DivU32 make(uint32_t d) {
+    DivU32 r;
+    int l = 0;
+    while ((1ull << l) < d) ++l;
+    r.s = l;
+    r.m = (uint32_t)((((1ull << l) - d) << 32) / d + 1);
+    return r;
+  }
+  __device__ __forceinline__ uint32_t div(uint32_t n) const { return (__umulhi(m, n) + n) >> s; }
+};
+
 struct Geom {
   int64_t B;    // local rows
   int64_t Bg;   // global rows (a-update constant)
   int T, D, H, O;
+  DivU32 dT{};  // by T; set with set_T() (B*T < 2^31 is checked at create)
   __host__ __device__ int64_t BT() const { return B * (int64_t)T; }
   __host__ __device__ int TP() const { return T + 1; }
+  void set_T() { dT = DivU32::make((uint32_t)T); }
+  // row (b, t) of the [B][T] grid -> row of the h plane [B][T+1] holding h_{t-1}: b*(T+1) + t
+  __device__ __forceinline__ int64_t hrow(int64_t row) const { return row + dT.div((uint32_t)row); }
 };
 
 struct Weights {            // model parameters, read in place (no packing)
@@ -48,6 +68,7 @@ struct DevStats {
   int pad;
   double f_w[8];
   double grad_sq[8];
+  double direct_frac[8];
 };
 
 // ---- time step (one t): GEMM [x_t | h_{t-1}] @ [Wx; Wh] for the 4 gates + fused epilogue

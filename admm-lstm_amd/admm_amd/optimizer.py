@@ -270,6 +270,7 @@ class AdmmOptimizerBase(object):
             'theta_h': s.theta_h,
             'unresolved': s.unresolved,
             'nonfinite': s.nonfinite,
+            'direct_frac': {name: s.direct_frac[i] for i, name in enumerate(WEIGHT_ORDER)},
         }
 
     def profile(self, classes=()) -> None:

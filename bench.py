@@ -230,6 +230,7 @@ def main():
             'cpu_baseline': cpu,
             'kernels': kernel_ms,
             'line_search_k': list(stats['k'].values()),
+            'direct_frac': [round(v, 4) for v in stats['direct_frac'].values()],
             'final_train_mse': loss,
         }
         print(json.dumps(out), flush=True)

@@ -91,6 +91,8 @@ typedef struct AdmmStats {
   float theta_h;              /* theta* of the h_T search (admm.py:474-482) */
   int32_t unresolved;         /* weight searches that hit the candidate cap (should be 0) */
   int32_t nonfinite;          /* NaN/Inf seen in line-search sums (should be 0) */
+  double direct_frac[8];      /* fraction of elements outside the polynomial regime of each
+                                 weight search (|q| > 2^-8: per-candidate evaluation) */
 } AdmmStats;
 
 typedef struct AdmmCtx AdmmCtx;

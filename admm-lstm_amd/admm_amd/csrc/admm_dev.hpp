@@ -37,76 +37,6 @@ __device__ __forceinline__ float sigm(float z) { return sig_pair(z).s; }
 
 __device__ __forceinline__ float act(bool is_tanh, float z) { return is_tanh ? tanhf(z) : sigm(z); }
 
-// ----------------------------------------------------------------------------- trial increments
-//
-// The line search needs D = phi(z + d) - phi(z) for d = q * 2^-k, k = 0..J-1, for every
-// element, where d is often far below ulp(z): the reference's f(beta) - f(W) is then
-// pure fp32 rounding noise (DESIGN.md "line-search numerics").  Per element we keep
-//   |d| <= 1/16 : 5-term Taylor series about z (no transcendental; truncation < 1e-7
-//                 relative: the series of sigma / tanh converge for |d| < pi, pi/2);
-//   |d| >  1/16 : phi(z+d) - phi(z) from fast v_exp/v_rcp, in the complement form
-//                 (1 - phi) when z > 0 so saturated gates do not cancel.
-struct TrialElem {
-  float z, d0;          // pre-activation, phi(z) - target
-  float c1, c2, c3, c4, c5;
-  float lo, hi;         // sigmoid: s, 1-s ; tanh: 1+u, 1-u  (accurate)
-};
-
-__device__ __forceinline__ TrialElem trial_elem_sigmoid(float z, float tgt) {
-  const SigPair sp = sig_pair(z);
-  const float p = sp.s * sp.sc, m = sp.sc - sp.s;
-  TrialElem e;
-  e.z = z;
-  e.d0 = sp.s - tgt;
-  e.c1 = p;
-  e.c2 = 0.5f * p * m;
-  e.c3 = p * (1.f - 6.f * p) * (1.f / 6.f);
-  e.c4 = p * m * (1.f - 12.f * p) * (1.f / 24.f);
-  e.c5 = p * (1.f + p * (-30.f + 120.f * p)) * (1.f / 120.f);
-  e.lo = sp.s;
-  e.hi = sp.sc;
-  return e;
-}
-
-__device__ __forceinline__ TrialElem trial_elem_tanh(float z, float tgt) {
-  const float ez = expf(-2.f * fabsf(z));
-  const float mz = 2.f * ez / (1.f + ez);        // 1 - |tanh z|
-  const float u = copysignf(1.f - mz, z);
-  const float t1 = mz * (2.f - mz);              // 1 - u^2 without cancellation
-  const float u2 = u * u;
-  TrialElem e;
-  e.z = z;
-  e.d0 = tanhf(z) - tgt;  // same tanh as the stored gate / residual (step-1 exactness)
-  e.c1 = t1;
-  e.c2 = -u * t1;
-  e.c3 = t1 * (u2 - (1.f / 3.f));
-  e.c4 = u * t1 * (2.f - 3.f * u2) * (1.f / 3.f);
-  e.c5 = t1 * (2.f + u2 * (-15.f + 15.f * u2)) * (1.f / 15.f);
-  e.lo = z < 0.f ? mz : 2.f - mz;                // 1 + u
-  e.hi = z < 0.f ? 2.f - mz : mz;                // 1 - u
-  return e;
-}
-
-__device__ __forceinline__ float fast_rcp(float x) { return __builtin_amdgcn_rcpf(x); }
-
-template <bool TANH>
-__device__ __forceinline__ float trial_delta(const TrialElem& e, float d) {
-  if (fabsf(d) <= 0.0625f) return d * (e.c1 + d * (e.c2 + d * (e.c3 + d * (e.c4 + d * e.c5))));
-  const float t = e.z + d;
-  if (!TANH) {
-    const float ex = __expf(-fabsf(t));
-    const float r = fast_rcp(1.f + ex);
-    const float st = t >= 0.f ? r : ex * r;       // sigma(t)
-    const float sct = t >= 0.f ? ex * r : r;      // 1 - sigma(t)
-    return e.z > 0.f ? (e.hi - sct) : (st - e.lo);
-  }
-  const float ex = __expf(-2.f * fabsf(t));
-  const float mt = 2.f * ex * fast_rcp(1.f + ex); // 1 - |tanh t|
-  const float lo_t = t < 0.f ? mt : 2.f - mt;     // 1 + tanh t
-  const float hi_t = t < 0.f ? 2.f - mt : mt;     // 1 - tanh t
-  return e.z > 0.f ? (e.hi - hi_t) : (lo_t - e.lo);
-}
-
 // ----------------------------------------------------------------------------- reductions
 
 __device__ __forceinline__ float wave_sum(float v) {

@@ -550,30 +550,91 @@ __global__ __launch_bounds__(kThreads) void k_qgemm(Geom g, const float* x, cons
 //    a_n = c_n q^n (3-term Taylor, truncation < 1e-8 relative for every k >= 0), so the
 //    increment is a degree-6 polynomial in s whose 6 coefficients are summed once (pass 0)
 //    and cover every exponent;
-//  * otherwise: D_k evaluated per candidate for the pass window k in [pass*J, pass*J + J)
-//    (5-term Taylor for |d| <= 1/16, cancellation-free direct form above).
+//  * otherwise: D_k per candidate of the pass window k in [pass*J, pass*J + J), branch-free
+//    (see trial_direct).
 // Slot layout per gate: kSlots = [J candidates][6 poly][sum d0^2][#per-candidate elements].
 constexpr int kSlots = kTrialSlots;
 constexpr int kSlotPoly = kTrialJ, kSlotFw = kTrialJ + kPolyN, kSlotNne = kTrialJ + kPolyN + 1;
 
+// expm1(x) to ~1 ulp: degree-8 Taylor on |x| < 1/2 (truncation < 2^-26 relative), else exp - 1
+__device__ __forceinline__ float expm1_acc(float x) {
+  if (fabsf(x) < 0.5f) {
+    float p = 1.f / 40320.f;
+    p = fmaf(p, x, 1.f / 5040.f);
+    p = fmaf(p, x, 1.f / 720.f);
+    p = fmaf(p, x, 1.f / 120.f);
+    p = fmaf(p, x, 1.f / 24.f);
+    p = fmaf(p, x, 1.f / 6.f);
+    p = fmaf(p, x, 0.5f);
+    p = fmaf(p, x, 1.f);
+    return p * x;
+  }
+  return __expf(x) - 1.f;
+}
+
+// Per-candidate increments of one element, all J candidates of the window, no branches.
+// With w = |z| (sigmoid) and sg = sign z, sigma(z + d) - sigma(z) = sg [sigma(w + e) - sigma(w)],
+// e = sg d, and with E = exp(-w), m = expm1(-e), y = E m:
+//   sigma(w + e) - sigma(w) = -sigma(w) y / (1 + E + y)
+// (no cancellation: m carries the difference).  tanh x = 2 sigma(2x) - 1 gives the tanh gate
+// with w = 2|z|, e = 2 sg d and a factor 2.  Along the window d halves, so
+// m_k = m_{k+1} (m_{k+1} + 2): one expm1 for the smallest d, then a multiply per candidate
+// (relative error grows < 1 ulp per step).  Where -e > 20, m = exp(-e) to 2e-9 and
+// y = exp(-e - w) is taken directly instead (E may underflow while y does not); y is capped
+// at 1e30, where y / (1 + E + y) = 1 (the saturated limit D = -sg sigma(w)).
+template <bool TANH>
+__device__ __forceinline__ void trial_direct(float z, float w, float E, float r, float d0, float qv, int pass,
+                                             float (&acc)[kSlots]) {
+  constexpr float kCap = 1e30f;
+  const float sg = z >= 0.f ? 1.f : -1.f;
+  const float f2 = TANH ? 2.f : 1.f;
+  const float cr = -(f2 * sg) * r;
+  float e = (f2 * sg) * qv * ldexpf(1.f, -(pass * kTrialJ + kTrialJ - 1));   // smallest candidate
+  float m = fminf(expm1_acc(-e), kCap);
+  const float one_e = 1.f + E, d2 = 2.f * d0;
+  if (fabsf(e) * (float)(1 << (kTrialJ - 1)) <= 20.f) {   // |e| <= 20 on every candidate: no exp
+#pragma unroll
+    for (int k = kTrialJ - 1; k >= 0; --k) {
+      const float y = E * m;
+      const float D = (cr * y) * __builtin_amdgcn_rcpf(one_e + y);
+      acc[k] = fmaf(D, d2 + D, acc[k]);
+      m = m * (m + 2.f);
+    }
+    return;
+  }
+#pragma unroll
+  for (int k = kTrialJ - 1; k >= 0; --k) {
+    const float yb = fminf(__expf(-e - w), kCap);
+    const float y = -e > 20.f ? yb : E * m;
+    const float D = (cr * y) * __builtin_amdgcn_rcpf(one_e + y);
+    acc[k] = fmaf(D, d2 + D, acc[k]);
+    m = fminf(m * (m + 2.f), kCap);
+    e *= 2.f;
+  }
+}
+
 template <bool TANH>
 __device__ __forceinline__ void trial_accumulate(float z, float tg, float qv, int pass, float (&acc)[kSlots]) {
+  // E = exp(-w), r = sigma(w), sc = 1 - sigma(w) on w = |z| (sigmoid) or 2|z| (tanh)
+  const float w = TANH ? 2.f * fabsf(z) : fabsf(z);
+  const float E = expf(-w);
+  const float r = 1.f / (1.f + E);
+  const float sc = E * r;
   float d0, c1, c2, c3;
   if (TANH) {
-    const float ez = expf(-2.f * fabsf(z));
-    const float mz = 2.f * ez / (1.f + ez);       // 1 - |tanh z|
+    const float mz = 2.f * sc;                    // 1 - |tanh z|
     const float u = copysignf(1.f - mz, z);
     c1 = mz * (2.f - mz);                         // 1 - u^2
     c2 = -u * c1;
     c3 = c1 * (u * u - (1.f / 3.f));
     d0 = tanhf(z) - tg;                           // the tanh of the stored gate / residual
   } else {
-    const SigPair sp = sig_pair(z);
-    const float p = sp.s * sp.sc;
+    const float s = z >= 0.f ? r : sc, s_c = z >= 0.f ? sc : r;   // = sig_pair(z)
+    const float p = s * s_c;
     c1 = p;
-    c2 = 0.5f * p * (sp.sc - sp.s);
+    c2 = 0.5f * p * (s_c - s);
     c3 = p * (1.f - 6.f * p) * (1.f / 6.f);
-    d0 = sp.s - tg;
+    d0 = s - tg;
   }
   acc[kSlotFw] += d0 * d0;
   if (fabsf(qv) <= 0x1p-8f) {
@@ -589,17 +650,10 @@ __device__ __forceinline__ void trial_accumulate(float z, float tg, float qv, in
     return;
   }
   acc[kSlotNne] += 1.f;
-  const TrialElem e = TANH ? trial_elem_tanh(z, tg) : trial_elem_sigmoid(z, tg);
-  float sc = ldexpf(1.f, -pass * kTrialJ);
-#pragma unroll
-  for (int k = 0; k < kTrialJ; ++k) {
-    const float D = trial_delta<TANH>(e, qv * sc);   // sc = 2^-(pass*J+k): exact scaling
-    acc[k] += D * (2.f * e.d0 + D);
-    sc *= 0.5f;
-  }
+  trial_direct<TANH>(z, w, E, r, d0, qv, pass, acc);
 }
 
-__device__ __forceinline__ void trial_block_store(float (&acc)[kSlots], double* part, int q, int nblk) {
+__device__ __forceinline__ void trial_block_store(float (&acc)[kSlots], double* part, int q, int blk, int nblk) {
   __shared__ double red[4][kSlots];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
 #pragma unroll
@@ -610,17 +664,17 @@ __device__ __forceinline__ void trial_block_store(float (&acc)[kSlots], double* 
   __syncthreads();
   if (threadIdx.x < kSlots) {
     const int k = threadIdx.x;
-    part[((int64_t)q * kSlots + k) * nblk + blockIdx.x] = (red[0][k] + red[1][k]) + (red[2][k] + red[3][k]);
+    part[((int64_t)q * kSlots + k) * nblk + blk] = (red[0][k] + red[1][k]) + (red[2][k] + red[3][k]);
   }
 }
 
 // Generic trial pass: materialised z (zc) and Q.
 template <bool TANH, int VEC>
 __device__ __forceinline__ void trial_loop(int64_t n, const float* zq, const float* tq, const float* Qq, int pass,
-                                           float (&acc)[kSlots]) {
+                                           int blk, int nblk, float (&acc)[kSlots]) {
   const int64_t nv = n / VEC;
-  const int64_t stride = (int64_t)gridDim.x * kThreads;
-  for (int64_t v = (int64_t)blockIdx.x * kThreads + threadIdx.x; v < nv; v += stride) {
+  const int64_t stride = (int64_t)nblk * kThreads;
+  for (int64_t v = (int64_t)blk * kThreads + threadIdx.x; v < nv; v += stride) {
     if (VEC == 4) {
       const float4 z4 = reinterpret_cast<const float4*>(zq)[v];
       const float4 t4 = reinterpret_cast<const float4*>(tq)[v];
@@ -640,7 +694,7 @@ __device__ __forceinline__ void trial_loop(int64_t n, const float* zq, const flo
 
 __global__ __launch_bounds__(kThreads) void k_trial(Geom g, int pass, const float* zc, const float* tgt,
                                                       const float* Q, const int* found, double* part, int nblk) {
-  const int q = blockIdx.y;
+  const int q = blockIdx.y, blk = blockIdx.x;  // gate-major: one code path per CU at a time (I-cache)
   if (found[q]) return;
   const int64_t n = g.BT() * g.H;
   const float* zq = zc + (int64_t)q * n;
@@ -651,13 +705,13 @@ __global__ __launch_bounds__(kThreads) void k_trial(Geom g, int pass, const floa
   for (int k = 0; k < kSlots; ++k) acc[k] = 0.f;
   const bool vec = (g.H % 4) == 0;
   if (q == 2) {
-    if (vec) trial_loop<true, 4>(n, zq, tq, Qq, pass, acc);
-    else trial_loop<true, 1>(n, zq, tq, Qq, pass, acc);
+    if (vec) trial_loop<true, 4>(n, zq, tq, Qq, pass, blk, nblk, acc);
+    else trial_loop<true, 1>(n, zq, tq, Qq, pass, blk, nblk, acc);
   } else {
-    if (vec) trial_loop<false, 4>(n, zq, tq, Qq, pass, acc);
-    else trial_loop<false, 1>(n, zq, tq, Qq, pass, acc);
+    if (vec) trial_loop<false, 4>(n, zq, tq, Qq, pass, blk, nblk, acc);
+    else trial_loop<false, 1>(n, zq, tq, Qq, pass, blk, nblk, acc);
   }
-  trial_block_store(acc, part, q, nblk);
+  trial_block_store(acc, part, q, blk, nblk);
 }
 
 // Fast trial pass (D <= kFastD, H % 4 == 0): rows x float4 columns.  Side 0 forms the trial
@@ -723,7 +777,8 @@ constexpr int kRPI = 2;
 template <bool TANH, int SIDE, int DP, bool XV>
 __device__ __forceinline__ void trial_fast_body(const Geom& g, int q, int pass, const float* __restrict__ zc,
                                                 const float* __restrict__ tgt, const float* __restrict__ Q,
-                                                const float* __restrict__ x, const float* Wlds, float (&acc)[kSlots]) {
+                                                const float* __restrict__ x, const float* Wlds, int blk, int nblk,
+                                                float (&acc)[kSlots]) {
   const int64_t BT = g.BT(), n = BT * g.H;
   const float* __restrict__ zq = zc + (int64_t)q * n;
   const float* __restrict__ tq = tgt + (int64_t)q * n;
@@ -732,8 +787,8 @@ __device__ __forceinline__ void trial_fast_body(const Geom& g, int q, int pass, 
   RowCols rc(g.H);
   if (rc.rr >= rc.rpb) return;
   const int j = 4 * rc.c4, H4 = g.H / 4;   // fast path: H/4 <= 256, one float4 column per thread
-  const int64_t stride = (int64_t)gridDim.x * rc.rpb;
-  for (int64_t row0 = (int64_t)blockIdx.x * rc.rpb + rc.rr; row0 < BT; row0 += kRPI * stride) {
+  const int64_t stride = (int64_t)nblk * rc.rpb;
+  for (int64_t row0 = (int64_t)blk * rc.rpb + rc.rr; row0 < BT; row0 += kRPI * stride) {
     float4 z4[kRPI], t4[kRPI], q4[kRPI];
     float xr[kRPI][DP];
 #pragma unroll
@@ -767,15 +822,15 @@ __global__ __launch_bounds__(kThreads) void k_trial_fast(Geom g, int pass, const
                                                            const float* Q, const float* x, const float* Wsrc,
                                                            const int* found, double* part, int nblk) {
   extern __shared__ float wlds[];  // [DP][H] (side 0 only)
-  const int q = blockIdx.y;
+  const int q = blockIdx.y, blk = blockIdx.x;  // gate-major: one code path per CU at a time (I-cache)
   if (found[q]) return;
   if (SIDE == 0) stage_wlds<DP>(g, Wsrc + (int64_t)q * g.D * g.H, wlds);
   float acc[kSlots];
 #pragma unroll
   for (int k = 0; k < kSlots; ++k) acc[k] = 0.f;
-  if (q == 2) trial_fast_body<true, SIDE, DP, XV>(g, q, pass, zc, tgt, Q, x, wlds, acc);
-  else trial_fast_body<false, SIDE, DP, XV>(g, q, pass, zc, tgt, Q, x, wlds, acc);
-  trial_block_store(acc, part, q, nblk);
+  if (q == 2) trial_fast_body<true, SIDE, DP, XV>(g, q, pass, zc, tgt, Q, x, wlds, blk, nblk, acc);
+  else trial_fast_body<false, SIDE, DP, XV>(g, q, pass, zc, tgt, Q, x, wlds, blk, nblk, acc);
+  trial_block_store(acc, part, q, blk, nblk);
 }
 
 // After the x stage: zc += X dWx, so the h stage sees z = X Wx_new + Hprev Wh
@@ -898,14 +953,14 @@ __global__ __launch_bounds__(kThreads) void k_trial_debug(int64_t n, int tanh_ga
   for (int k = 0; k < kSlots; ++k) acc[k] = 0.f;
   const int pass = kbase / kTrialJ;
   // the polynomial slots are only filled on pass 0: run pass 0 for them, then this pass
-  if (tanh_gate) trial_loop<true, 1>(n, z, tgt, qv, 0, acc);
-  else trial_loop<false, 1>(n, z, tgt, qv, 0, acc);
+  if (tanh_gate) trial_loop<true, 1>(n, z, tgt, qv, 0, blockIdx.x, gridDim.x, acc);
+  else trial_loop<false, 1>(n, z, tgt, qv, 0, blockIdx.x, gridDim.x, acc);
   if (pass > 0) {
     float acc2[kSlots];
 #pragma unroll
     for (int k = 0; k < kSlots; ++k) acc2[k] = 0.f;
-    if (tanh_gate) trial_loop<true, 1>(n, z, tgt, qv, pass, acc2);
-    else trial_loop<false, 1>(n, z, tgt, qv, pass, acc2);
+    if (tanh_gate) trial_loop<true, 1>(n, z, tgt, qv, pass, blockIdx.x, gridDim.x, acc2);
+    else trial_loop<false, 1>(n, z, tgt, qv, pass, blockIdx.x, gridDim.x, acc2);
 #pragma unroll
     for (int k = 0; k < kTrialJ; ++k) acc[k] = acc2[k];
   }

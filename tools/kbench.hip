@@ -66,6 +66,15 @@ int main(int argc, char** argv) {
   timeit("apply_dwx", 2 * f4 * 4 * n + f4 * BT * g.D, 0, [&] { launch_apply_dwx(g, x, dW, zc, s); });
   timeit("trial_fast side0", f4 * 2 * 4 * n, 0, [&] { launch_trial_fast(g, 0, 0, zc, tgt, nullptr, x, G, found, part, nb, s); });
   timeit("trial_fast side1", f4 * 3 * 4 * n, 0, [&] { launch_trial_fast(g, 1, 0, zc, tgt, Q, x, dW, found, part, nb, s); });
+  {
+    float* G0; (void)hipMalloc(&G0, 4 * g.H * g.H * 4); (void)hipMemset(G0, 0, 4 * g.H * g.H * 4);
+    timeit("trial_fast side0 q=0", f4 * 2 * 4 * n, 0, [&] { launch_trial_fast(g, 0, 0, zc, tgt, nullptr, x, G0, found, part, nb, s); });
+    float* Qb = dev_random(4 * n, -1.f, 1.f, 7);
+    timeit("trial_fast side1 |q|<1", f4 * 3 * 4 * n, 0, [&] { launch_trial_fast(g, 1, 0, zc, tgt, Qb, x, dW, found, part, nb, s); });
+    float* Qm = dev_random(4 * n, -0.01f, 0.01f, 8);
+    timeit("trial_fast side1 |q|<.01", f4 * 3 * 4 * n, 0, [&] { launch_trial_fast(g, 1, 0, zc, tgt, Qm, x, dW, found, part, nb, s); });
+    (void)hipFree(Qb); (void)hipFree(Qm); (void)hipFree(G0);
+  }
   timeit("trial generic", f4 * 3 * 4 * n, 0, [&] { launch_trial(g, 0, zc, tgt, Q, found, part, trial_blocks(g), s); });
   timeit("resid_gx", f4 * 4 * 4 * n, 0, [&] { launch_resid_gx(g, hp, x, S, L, zc, tgt, slab, resid_gx_blocks(g), s); });
   const int ns = atr_splits(g, 1);

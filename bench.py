@@ -80,6 +80,27 @@ def roofline_terms(cls: str, B: int, T: int, D: int, H: int):
     return None
 
 
+# kernel symbols of each profile class (admm_kernels.hip), for the committed PMC traffic
+CLASS_KERNELS = {'sweep': ('k_sweep_t',), 'atr_h': ('k_atr_fused', 'k_atr<128'), 'qgemm_h': ('k_qgemm<true, 1>',),
+                 'trial': ('k_trial_fast', 'k_trial<'), 'resid': ('k_resid_gx', 'k_apply_dwx', 'k_resid<')}
+
+
+def pmc_traffic(cls: str, cfg_name: str):
+    """HBM bytes per launch of a kernel class from the newest committed PMC summary
+    (profiles/r*_pmc_<cfg>.json, written by tools/pmc_to_json.py from rocprofv3 FETCH_SIZE /
+    WRITE_SIZE passes of this same bench command), or None if there is none."""
+    import glob
+    import json
+    files = sorted(glob.glob(os.path.join(ROOT, 'profiles', f'r*_pmc_{cfg_name}.json')))
+    if not files or cls not in CLASS_KERNELS:
+        return None
+    kern = json.load(open(files[-1]))['kernels']
+    # trial passes after the first return early (gates already decided): use the full pass
+    key = 'traffic_bytes_max' if cls == 'trial' else 'traffic_bytes_median'
+    vals = [v[key] for k, v in kern.items() if k.startswith(CLASS_KERNELS[cls])]
+    return sum(vals) / len(vals) if vals else None
+
+
 def cpu_baseline(cfg_name: str, seconds_hint: float = 20.0):
     """Time the CPU oracle (reference op structure) on a bounded sample of the workload."""
     from oracle import admm_oracle as O
@@ -203,7 +224,10 @@ def main():
         else:
             roof = {'bound': 'hbm', 'achieved': nbytes / avg_s / 1e9, 'peak': PEAK_HBM / 1e9, 'unit': 'GB/s'}
         roof['frac'] = roof['achieved'] / roof['peak']
-        roof['traffic'] = None
+        # traffic: measured HBM bytes per launch (PMC, DESIGN.md "Measurement"), next to the
+        # algorithmic bytes per launch it should match
+        roof['traffic'] = pmc_traffic(cls, args.config)
+        roof['algorithmic_bytes'] = nbytes
         roof['kernel'] = cls
         roof['avg_launch_us'] = avg_s * 1e6
         roof['launches'] = n

@@ -70,6 +70,7 @@ struct AdmmCtx {
   double *tr_part = nullptr, *tr_sums = nullptr, *tr_poly = nullptr;
   int nblk_resid = 1, nblk_trial = 1, nblk_rx = 1;
   int* found = nullptr;
+  int* pick = nullptr;
   float *U = nullptr, *wy_slab = nullptr, *Gy = nullptr;
   int wy_nsplit = 1;
   double *ht_part = nullptr, *ht_sums = nullptr;
@@ -220,6 +221,7 @@ int stage_weights(AdmmCtx* c, int side, hipStream_t s) {
   for (int q = 0; q < 4; ++q) sa.W[q] = side == 0 ? c->buf.wx[q] : c->buf.wh[q];
   sa.dW = side == 0 ? c->dW : nullptr;
   sa.found = c->found;
+  sa.pick = c->pick;
   sa.stats = c->stats;
   const int nblk = fast ? stream_blocks(g) : c->nblk_trial;
   for (int pass = 0; pass < kMaxPasses; ++pass) {
@@ -333,7 +335,7 @@ int admm_create(const AdmmDims* dims, const AdmmParams* params, int device, Admm
       (rc = dalloc(&c->gslab, slab)) ||
       (rc = dalloc(&c->tr_part, (size_t)4 * kTrialSlots * c->nblk_trial)) ||
       (rc = dalloc(&c->tr_sums, (size_t)4 * kTrialSlots)) || (rc = dalloc(&c->tr_poly, (size_t)4 * kPolyN)) ||
-      (rc = dalloc(&c->found, 4)) ||
+      (rc = dalloc(&c->found, 4)) || (rc = dalloc(&c->pick, 4)) ||
       (rc = dalloc(&c->U, (size_t)g.B * g.O)) || (rc = dalloc(&c->wy_slab, (size_t)c->wy_nsplit * g.H * g.O)) ||
       (rc = dalloc(&c->Gy, (size_t)g.H * g.O)) || (rc = dalloc(&c->ht_part, (size_t)c->ht_nblk * kHTSums)) ||
       (rc = dalloc(&c->ht_sums, kHTSums)) || (rc = dalloc(&c->stats, 1))) {
@@ -352,7 +354,7 @@ int admm_create(const AdmmDims* dims, const AdmmParams* params, int device, Admm
 int admm_destroy(AdmmCtx* c) {
   if (!c) return ADMM_OK;
   (void)hipSetDevice(c->device);
-  void* ptrs[] = {c->zc, c->tgt, c->R, c->Q, c->G, c->dW, c->gslab, c->tr_part, c->tr_sums, c->tr_poly, c->found,
+  void* ptrs[] = {c->zc, c->tgt, c->R, c->Q, c->G, c->dW, c->gslab, c->tr_part, c->tr_sums, c->tr_poly, c->found, c->pick,
                   c->U, c->wy_slab, c->Gy, c->ht_part, c->ht_sums, c->stats};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);

@@ -1001,16 +1001,28 @@ __global__ __launch_bounds__(kThreads) void k_trial_reduce(int pass, const doubl
 // lhs_k = 0.5 rho (per-candidate sum of this window + polynomial part at s = 2^-k);
 // rhs_k = est_k - f(W) = sum G (beta - W) + 0.5 T theta ||beta - W||^2 = (1 + T/2) ||G||^2 2^-k.
 // If every element was in the polynomial regime the decision extends over all k < kMaxK.
-__global__ __launch_bounds__(kThreads) void k_select(Geom g, Hyper hp, SelectArgs a) {
+// Selection of one pass (admm.py:331-338): per gate, the first exponent k of the window with
+// f(W + G/2^k) - f(W) <= (1 + T/2) ||G||^2 2^-k, in fp64 from the pass sums.
+__global__ __launch_bounds__(kThreads) void k_decide(Geom g, Hyper hp, SelectArgs a) {
   __shared__ double red[4];
-  __shared__ int pick_s;
   const int q = blockIdx.x;
-  if (a.found[q]) return;
+  if (a.found[q]) {   // decided in an earlier pass
+    if (threadIdx.x == 0) a.pick[q] = -1;
+    return;
+  }
   const int Kd = a.side == 0 ? g.D : g.H;
   const int64_t nW = (int64_t)Kd * g.H;
   const float* Gq = a.G + (int64_t)q * nW;
   double gs = 0.0;
-  for (int64_t i = threadIdx.x; i < nW; i += kThreads) gs += (double)Gq[i] * (double)Gq[i];
+  if ((nW & 3) == 0) {
+    const float4* G4 = reinterpret_cast<const float4*>(Gq);
+    for (int64_t i = threadIdx.x; i < nW / 4; i += kThreads) {
+      const float4 v = G4[i];
+      gs += ((double)v.x * v.x + (double)v.y * v.y) + ((double)v.z * v.z + (double)v.w * v.w);
+    }
+  } else {
+    for (int64_t i = threadIdx.x; i < nW; i += kThreads) gs += (double)Gq[i] * (double)Gq[i];
+  }
   const double gsq = block_sum(gs, red);
   const float rho = hp.rho[q];
   if (threadIdx.x == 0) {
@@ -1046,17 +1058,26 @@ __global__ __launch_bounds__(kThreads) void k_select(Geom g, Hyper hp, SelectArg
       a.stats->passes[a.side] = a.pass + 1;
       a.found[q] = 1;
     }
-    pick_s = pick;
+    a.pick[q] = pick;
   }
-  __syncthreads();
-  const int pick = pick_s;
+}
+
+// W <- (0.5 rho T theta* W - G) / (beta + 0.5 rho theta* T), theta* = 2^k / 2 (admm.py:338-343),
+// for the gates decided in this pass; grid (blocks, 4).
+__global__ __launch_bounds__(kThreads) void k_wupdate(Geom g, Hyper hp, SelectArgs a) {
+  const int q = blockIdx.y;
+  const int pick = a.pick[q];
   if (pick < 0) return;
+  const int Kd = a.side == 0 ? g.D : g.H;
+  const int64_t nW = (int64_t)Kd * g.H;
+  const float* Gq = a.G + (int64_t)q * nW;
+  const float rho = hp.rho[q];
   const float theta = ldexpf(1.f, pick - 1);
   const float beta = a.side == 0 ? hp.beta_x[q] : hp.beta_h[q];
   const float c1 = ((0.5f * rho) * (float)g.T) * theta;
   const float den = beta + ((0.5f * rho) * theta) * (float)g.T;
   float* W = a.W[q];
-  for (int64_t i = threadIdx.x; i < nW; i += kThreads) {
+  for (int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x; i < nW; i += (int64_t)gridDim.x * kThreads) {
     const float w0 = W[i];
     const float w1 = (c1 * w0 - Gq[i]) / den;
     W[i] = w1;
@@ -1468,7 +1489,10 @@ void launch_trial_fast(const Geom& g, int side, int pass, const float* zc, const
 }
 
 void launch_select(const Geom& g, const Hyper& hp, const SelectArgs& a, hipStream_t s) {
-  k_select<<<4, kThreads, 0, s>>>(g, hp, a);
+  k_decide<<<4, kThreads, 0, s>>>(g, hp, a);
+  const int64_t nW = (int64_t)(a.side == 0 ? g.D : g.H) * g.H;
+  dim3 grid(std::max(1, std::min(cdiv64(nW, kThreads * 4), 256)), 4);
+  k_wupdate<<<grid, kThreads, 0, s>>>(g, hp, a);
 }
 
 int wy_splits(const Geom& g) {

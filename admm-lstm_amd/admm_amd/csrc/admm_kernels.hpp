@@ -158,6 +158,7 @@ struct SelectArgs {
   float* W[4];              // weights being updated (in place)
   float* dW;                // [4][K][H] W_new - W_old (side 0), nullable
   int* found;
+  int* pick;                // [4] exponent chosen in this pass, -1 if none (k_decide -> k_wupdate)
   DevStats* stats;
 };
 void launch_select(const Geom& g, const Hyper& hp, const SelectArgs& a, hipStream_t s);

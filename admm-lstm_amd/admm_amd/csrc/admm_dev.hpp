@@ -15,6 +15,7 @@
 namespace admm {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int kWave = 64;
 constexpr int kThreads = 256;  // every kernel: 4 waves per workgroup

@@ -8,6 +8,7 @@
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <algorithm>
 #include <string>
@@ -71,6 +72,9 @@ struct AdmmCtx {
   int nblk_resid = 1, nblk_trial = 1, nblk_rx = 1;
   int* found = nullptr;
   int* pick = nullptr;
+  int sweep_split = 1;     // sweep halves on two streams (ADMM_SWEEP_SPLIT=0: one stream)
+  hipStream_t s2 = nullptr;
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   float *U = nullptr, *wy_slab = nullptr, *Gy = nullptr;
   int wy_nsplit = 1;
   double *ht_part = nullptr, *ht_sums = nullptr;
@@ -251,9 +255,30 @@ int stage_sweep(AdmmCtx* c, hipStream_t s) {
   sa.S = planes(c->buf.gates);
   sa.L = planes(c->buf.duals);
   sa.zc = c->zc;
-  for (int t = 1; t <= g.T; ++t) {
+  {
+    // Samples are independent across the sweep: two halves on two streams run their
+    // per-t kernels concurrently, so one half's HBM-bound epilogue overlaps the other's
+    // MFMA-bound GEMM on the same CUs (one kernel per t alone runs them back to back).
     ProfScope ps(c, ADMM_PROF_SWEEP, s);
-    launch_sweep_t(g, t, w, c->hp, sa, s);
+    const int64_t mid = c->sweep_split ? std::min<int64_t>((g.B / 2 + 127) / 128 * 128, g.B) : g.B;
+    if (mid < g.B) {
+      HIP_TRY(hipEventRecord(c->ev_fork, s));
+      HIP_TRY(hipStreamWaitEvent(c->s2, c->ev_fork, 0));
+    }
+    for (int t = 1; t <= g.T; ++t) {
+      sa.r0 = 0;
+      sa.r1 = mid;
+      launch_sweep_t(g, t, w, c->hp, sa, s);
+      if (mid < g.B) {
+        sa.r0 = mid;
+        sa.r1 = g.B;
+        launch_sweep_t(g, t, w, c->hp, sa, c->s2);
+      }
+    }
+    if (mid < g.B) {
+      HIP_TRY(hipEventRecord(c->ev_join, c->s2));
+      HIP_TRY(hipStreamWaitEvent(s, c->ev_join, 0));
+    }
   }
   ProfScope ps(c, ADMM_PROF_SMALL, s);
   launch_ht_partial(g, c->hp, sa.S, sa.L, c->buf.a, c->buf.dual_y, c->buf.wy, c->ht_part, c->ht_nblk, s);
@@ -309,6 +334,7 @@ int admm_create(const AdmmDims* dims, const AdmmParams* params, int device, Admm
   g.H = dims->hidden_size;
   g.O = dims->output_size;
   g.set_T();
+  if (const char* e = std::getenv("ADMM_SWEEP_SPLIT")) c->sweep_split = std::atoi(e) != 0;
   Hyper& h = c->hp;
   for (int i = 0; i < 7; ++i) h.rho[i] = params->rho[i];
   for (int q = 0; q < 4; ++q) {
@@ -343,6 +369,12 @@ int admm_create(const AdmmDims* dims, const AdmmParams* params, int device, Admm
     admm_destroy(c);
     return fail(rc, "%s", msg.c_str());
   }
+  if (hipStreamCreateWithFlags(&c->s2, hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming) != hipSuccess) {
+    admm_destroy(c);
+    return fail(ADMM_EHIP, "stream/event creation failed");
+  }
   if (hipMemset(c->stats, 0, sizeof(DevStats)) != hipSuccess) {
     admm_destroy(c);
     return fail(ADMM_EHIP, "hipMemset(stats) failed");
@@ -360,6 +392,9 @@ int admm_destroy(AdmmCtx* c) {
     if (p) (void)hipFree(p);
   if (c->comm) ncclCommDestroy(c->comm);
   for (hipEvent_t e : c->ev_pool) (void)hipEventDestroy(e);
+  if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
+  if (c->ev_join) (void)hipEventDestroy(c->ev_join);
+  if (c->s2) (void)hipStreamDestroy(c->s2);
   for (auto& u : c->ev_used) {
     (void)hipEventDestroy(u.second.first);
     (void)hipEventDestroy(u.second.second);

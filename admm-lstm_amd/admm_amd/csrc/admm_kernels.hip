@@ -16,6 +16,20 @@ namespace {
 
 inline int cdiv64(int64_t a, int64_t b) { return (int)((a + b - 1) / b); }
 
+// Calls f(integral_constant<DP>, integral_constant<XV>) for the padded input width of g.
+template <class F>
+void with_dp(const Geom& g, F&& f) {
+  using std::integral_constant;
+  const bool xv = (g.D % 4) == 0;
+  switch ((g.D + 3) / 4) {
+    case 1: xv ? f(integral_constant<int, 4>{}, std::true_type{}) : f(integral_constant<int, 4>{}, std::false_type{}); break;
+    case 2: xv ? f(integral_constant<int, 8>{}, std::true_type{}) : f(integral_constant<int, 8>{}, std::false_type{}); break;
+    case 3: xv ? f(integral_constant<int, 12>{}, std::true_type{}) : f(integral_constant<int, 12>{}, std::false_type{}); break;
+    default: xv ? f(integral_constant<int, 16>{}, std::true_type{}) : f(integral_constant<int, 16>{}, std::false_type{}); break;
+  }
+}
+
+
 // ============================================================================ time step
 // Tile: 128 rows (samples) x 128 columns = 4 gates x 32 hidden units; each wave owns 32
 // rows x all 4 gates, so gate q's pre-activation of (b, j) sits in the same lane for every
@@ -75,8 +89,9 @@ struct StepSrc {  // A = [x_t | h_{t-1}] rows (row-major, K = D + H)
 
 template <bool VEC>
 __device__ __forceinline__ void step_gemm(const Geom& g, int t, const Weights& w, const float* hprev, int64_t hstride,
-                                          const float* x, f32x16 (&acc)[1][4], float* smem, int64_t m0, int j0) {
-  StepSrc<VEC> src{x + (int64_t)(t - 1) * g.D, (int64_t)g.T * g.D, hprev, hstride, g.B, g.D, g.H, w, j0};
+                                          const float* x, f32x16 (&acc)[1][4], float* smem, int64_t m0, int j0,
+                                          int64_t rend) {
+  StepSrc<VEC> src{x + (int64_t)(t - 1) * g.D, (int64_t)g.T * g.D, hprev, hstride, rend, g.D, g.H, w, j0};
   Engine<TS_BM, TS_BN, TS_WM, TS_WN, TS_KC, StepSrc<VEC>> eng;
   eng.run(src, m0, 0, 0, g.D + g.H, acc, smem);
 }
@@ -90,7 +105,7 @@ __global__ __launch_bounds__(kThreads) void k_forward_t(Geom g, int t, Weights w
   const int j0 = (lid % nj) * 32;
   f32x16 acc[1][4];
   zero_acc(acc);
-  step_gemm<VEC>(g, t, w, a.hprev, a.hprev_stride, a.x, acc, smem, m0, j0);
+  step_gemm<VEC>(g, t, w, a.hprev, a.hprev_stride, a.x, acc, smem, m0, j0, g.B);
   const int lane = threadIdx.x & 63, wm0 = (threadIdx.x >> 6) * TS_WM;
   const int j = j0 + (lane & 31);
   if (j >= g.H) return;
@@ -119,6 +134,53 @@ __global__ __launch_bounds__(kThreads) void k_forward_t(Geom g, int t, Weights w
   }
 }
 
+// ---- one (b, j) point of the time sweep: i, f, g, o (admm.py:353-386), c (388-436),
+// h for t < T (455-457), duals of i, f, g, o, c (504-530).  Operand grouping follows the
+// reference expression by expression (fp32).
+struct SweepIn {
+  float zi, zf, zg, zo;       // pre-activations x_t Wx_q + h_{t-1} Wh_q
+  float f0, g0, c0, h0, cp;   // old f, g, c, h at t; new c at t-1
+  float li, lf, lg, lo, lc, lh;
+};
+struct SweepRes {
+  float i1, f1, g1, o1, c1, h1;
+  float li, lf, lg, lo, lc;
+};
+
+__device__ __forceinline__ SweepRes sweep_point(const Hyper& hp, const SweepIn& v, bool last) {
+  const float ri = hp.rho[0], rf = hp.rho[1], rg = hp.rho[2], ro = hp.rho[3], rc = hp.rho[4], rh = hp.rho[5];
+  const float ai = sigm(v.zi), af = sigm(v.zf), ag = tanhf(v.zg), ao = sigm(v.zo);
+  const float f0 = v.f0, g0 = v.g0, c0 = v.c0, h0 = v.h0, cp = v.cp;
+  const float li = v.li, lf = v.lf, lg = v.lg, lo = v.lo, lc = v.lc, lh = v.lh;
+  SweepRes o;
+  // admm.py:384-386 with (p1,p2,p3) of :360-375 and (var2, rho2, lam2) of :376-383
+  o.i1 = -((li - ri * ai) + (rc * (f0 * cp - c0) - lc) * g0) / (ri + rc * g0 * g0);
+  o.f1 = -((lf - rf * af) + (rc * (g0 * o.i1 - c0) - lc) * cp) / (rf + rc * cp * cp);
+  o.g1 = -((lg - rg * ag) + (rc * (o.f1 * cp - c0) - lc) * o.i1) / (rg + rc * o.i1 * o.i1);
+  const float tc0 = tanhf(c0);
+  o.o1 = -((lo - ro * ao) + (rh * (0.f - h0) - lh) * tc0) / (ro + rh * tc0 * tc0);
+  // admm.py:388-436: autograd gradient of .5||tanh(c) o - (h + lam_h/rho_h)||^2, theta* = 0.5
+  const float div_h = lh / rh, div_c = lc / rc;
+  const float vv = tc0 * o.o1 - (h0 + div_h);
+  const float gc = (vv * o.o1) * (1.f - tc0 * tc0);
+  const float A = (div_c - o.f1 * cp) - o.i1 * o.g1;
+  o.c1 = (0.5f * c0 - gc - rc * A) / (rc + 0.5f);
+  o.h1 = last ? h0 : (rh * o.o1 * tanhf(o.c1) - lh) / rh;  // admm.py:455-457
+  // admm.py:512-530
+  o.li = li + ri * (o.i1 - ai);
+  o.lf = lf + rf * (o.f1 - af);
+  o.lg = lg + rg * (o.g1 - ag);
+  o.lo = lo + ro * (o.o1 - ao);
+  o.lc = lc + rc * (o.c1 - (o.f1 * cp + o.i1 * o.g1));
+  return o;
+}
+
+__device__ __forceinline__ void sweep_store(const SweepT& a, const SweepRes& o, int64_t ot, bool last) {
+  a.S.p[0][ot] = o.i1; a.S.p[1][ot] = o.f1; a.S.p[2][ot] = o.g1; a.S.p[3][ot] = o.o1; a.S.p[4][ot] = o.c1;
+  if (!last) a.S.p[5][ot] = o.h1;
+  a.L.p[0][ot] = o.li; a.L.p[1][ot] = o.lf; a.L.p[2][ot] = o.lg; a.L.p[3][ot] = o.lo; a.L.p[4][ot] = o.lc;
+}
+
 // One ADMM time step t (admm.py:72-76): i, f, g, o (admm.py:353-386), c (388-436),
 // h for t < T (455-457), dual ascent for i, f, g, o, c (504-530).  h_T, a and the
 // duals of h at T are finished by the h_T kernels below.
@@ -127,53 +189,33 @@ __global__ __launch_bounds__(kThreads) void k_sweep_t(Geom g, int t, Weights w, 
   __shared__ float smem[TSTile::LDS_FLOATS];
   const int nj = (g.H + 31) / 32;
   const int lid = xcd_swizzle(blockIdx.x, gridDim.x);
-  const int64_t m0 = (int64_t)(lid / nj) * TS_BM;
+  const int64_t m0 = a.r0 + (int64_t)(lid / nj) * TS_BM;
   const int j0 = (lid % nj) * 32;
   const int64_t rs = (int64_t)g.TP() * g.H;  // row stride of a [B,T+1,H] plane
   f32x16 acc[1][4];
   zero_acc(acc);
-  step_gemm<VEC>(g, t, w, a.S.p[5] + (int64_t)(t - 1) * g.H, rs, a.x, acc, smem, m0, j0);
+  step_gemm<VEC>(g, t, w, a.S.p[5] + (int64_t)(t - 1) * g.H, rs, a.x, acc, smem, m0, j0, a.r1);
   const int lane = threadIdx.x & 63, wm0 = (threadIdx.x >> 6) * TS_WM;
   const int j = j0 + (lane & 31);
   if (j >= g.H) return;
   const int64_t BT = g.BT();
-  const float ri = hp.rho[0], rf = hp.rho[1], rg = hp.rho[2], ro = hp.rho[3], rc = hp.rho[4], rh = hp.rho[5];
   const bool last = (t == g.T);
-  float *Si = a.S.p[0], *Sf = a.S.p[1], *Sg = a.S.p[2], *So = a.S.p[3], *Sc = a.S.p[4], *Sh = a.S.p[5];
-  float *Li = a.L.p[0], *Lf = a.L.p[1], *Lg = a.L.p[2], *Lo = a.L.p[3], *Lc = a.L.p[4], *Lh = a.L.p[5];
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
     const int64_t b = m0 + wm0 + acc_row(r, lane);
-    if (b >= g.B) continue;
+    if (b >= a.r1) continue;
     const int64_t ot = b * rs + (int64_t)t * g.H + j;
     const int64_t op = ot - g.H;
-    const float zi = acc[0][0][r], zf = acc[0][1][r], zg = acc[0][2][r], zo = acc[0][3][r];
-    const float ai = sigm(zi), af = sigm(zf), ag = tanhf(zg), ao = sigm(zo);
-    const float f0 = Sf[ot], g0 = Sg[ot], c0 = Sc[ot], h0 = Sh[ot];
-    const float cp = Sc[op];
-    const float li = Li[ot], lf = Lf[ot], lg = Lg[ot], lo = Lo[ot], lc = Lc[ot], lh = Lh[ot];
-    // admm.py:384-386 with (p1,p2,p3) of :360-375 and (var2, rho2, lam2) of :376-383
-    const float i1 = -((li - ri * ai) + (rc * (f0 * cp - c0) - lc) * g0) / (ri + rc * g0 * g0);
-    const float f1 = -((lf - rf * af) + (rc * (g0 * i1 - c0) - lc) * cp) / (rf + rc * cp * cp);
-    const float g1 = -((lg - rg * ag) + (rc * (f1 * cp - c0) - lc) * i1) / (rg + rc * i1 * i1);
-    const float tc0 = tanhf(c0);
-    const float o1 = -((lo - ro * ao) + (rh * (0.f - h0) - lh) * tc0) / (ro + rh * tc0 * tc0);
-    // admm.py:388-436: autograd gradient of .5||tanh(c) o - (h + lam_h/rho_h)||^2, theta* = 0.5
-    const float div_h = lh / rh, div_c = lc / rc;
-    const float v = tc0 * o1 - (h0 + div_h);
-    const float gc = (v * o1) * (1.f - tc0 * tc0);
-    const float A = (div_c - f1 * cp) - i1 * g1;
-    const float c1 = (0.5f * c0 - gc - rc * A) / (rc + 0.5f);
-    Si[ot] = i1; Sf[ot] = f1; Sg[ot] = g1; So[ot] = o1; Sc[ot] = c1;
-    if (!last) Sh[ot] = (rh * o1 * tanhf(c1) - lh) / rh;  // admm.py:455-457
-    // admm.py:512-530
-    Li[ot] = li + ri * (i1 - ai);
-    Lf[ot] = lf + rf * (f1 - af);
-    Lg[ot] = lg + rg * (g1 - ag);
-    Lo[ot] = lo + ro * (o1 - ao);
-    Lc[ot] = lc + rc * (c1 - (f1 * cp + i1 * g1));
+    SweepIn v;
+    v.zi = acc[0][0][r]; v.zf = acc[0][1][r]; v.zg = acc[0][2][r]; v.zo = acc[0][3][r];
+    v.f0 = a.S.p[1][ot]; v.g0 = a.S.p[2][ot]; v.c0 = a.S.p[4][ot]; v.h0 = a.S.p[5][ot];
+    v.cp = a.S.p[4][op];
+    v.li = a.L.p[0][ot]; v.lf = a.L.p[1][ot]; v.lg = a.L.p[2][ot]; v.lo = a.L.p[3][ot];
+    v.lc = a.L.p[4][ot]; v.lh = a.L.p[5][ot];
+    const SweepRes o = sweep_point(hp, v, last);
+    sweep_store(a, o, ot, last);
     const int64_t e = (b * g.T + (t - 1)) * g.H + j;
-    a.zc[e] = zi; a.zc[BT * g.H + e] = zf; a.zc[2 * BT * g.H + e] = zg; a.zc[3 * BT * g.H + e] = zo;
+    a.zc[e] = v.zi; a.zc[BT * g.H + e] = v.zf; a.zc[2 * BT * g.H + e] = v.zg; a.zc[3 * BT * g.H + e] = v.zo;
   }
 }
 
@@ -1328,7 +1370,7 @@ void launch_forward_t(const Geom& g, int t, const Weights& w, const ForwardT& a,
 }
 
 void launch_sweep_t(const Geom& g, int t, const Weights& w, const Hyper& hp, const SweepT& a, hipStream_t s) {
-  dim3 grid(cdiv64(g.B, TS_BM) * cdiv64(g.H, 32));
+  dim3 grid(cdiv64(a.r1 - a.r0, TS_BM) * cdiv64(g.H, 32));
   if (vec_ok(g)) k_sweep_t<true><<<grid, kThreads, 0, s>>>(g, t, w, hp, a);
   else k_sweep_t<false><<<grid, kThreads, 0, s>>>(g, t, w, hp, a);
 }
@@ -1428,19 +1470,6 @@ bool fast_path(const Geom& g) {
 int resid_gx_blocks(const Geom& g) {
   int nb = cdiv64(g.BT(), 256);
   return nb > 256 ? 256 : (nb < 1 ? 1 : nb);
-}
-
-// Calls f(integral_constant<DP>, integral_constant<XV>) for the padded input width of g.
-template <class F>
-void with_dp(const Geom& g, F&& f) {
-  using std::integral_constant;
-  const bool xv = (g.D % 4) == 0;
-  switch ((g.D + 3) / 4) {
-    case 1: xv ? f(integral_constant<int, 4>{}, std::true_type{}) : f(integral_constant<int, 4>{}, std::false_type{}); break;
-    case 2: xv ? f(integral_constant<int, 8>{}, std::true_type{}) : f(integral_constant<int, 8>{}, std::false_type{}); break;
-    case 3: xv ? f(integral_constant<int, 12>{}, std::true_type{}) : f(integral_constant<int, 12>{}, std::false_type{}); break;
-    default: xv ? f(integral_constant<int, 16>{}, std::true_type{}) : f(integral_constant<int, 16>{}, std::false_type{}); break;
-  }
 }
 
 size_t fast_lds(const Geom& g) { return (size_t)((g.D + 3) / 4) * 4 * g.H * sizeof(float); }

@@ -87,8 +87,10 @@ struct SweepT {
   const float* x;
   Planes6 S, L;             // [B,T+1,H] each
   float* zc;                // [4][B*T][H]: z cache for the next step's first weight stage
+  int64_t r0, r1;           // sample rows [r0, r1) of this launch
 };
 void launch_sweep_t(const Geom& g, int t, const Weights& w, const Hyper& hp, const SweepT& a, hipStream_t s);
+
 
 // out[b][o] = h_row(b) . wy[:, o]
 void launch_rowdot(int64_t B, int H, int O, const float* h, int64_t h_stride, const float* wy, float* out,

@@ -62,8 +62,8 @@ def make_data(gen: str, B: int, T: int, D: int, seed_offset: int = 0):
 def roofline_terms(cls: str, B: int, T: int, D: int, H: int):
     """Algorithmic (flops, bytes) of ONE launch of a kernel class."""
     f4 = 4  # bytes per fp32
-    if cls == 'sweep':            # one time step: [B, D+H] x [D+H, 4H] + fused gate/dual updates
-        return 2.0 * B * (D + H) * 4 * H, f4 * B * (D + 27 * H)
+    if cls == 'sweep':            # whole sweep t = 1..T: per t [B, D+H] x [D+H, 4H] + fused gate/dual updates
+        return T * 2.0 * B * (D + H) * 4 * H, T * f4 * B * (D + 27 * H)
     n = float(B) * T * H          # elements of one [B*T, H] plane
     if cls == 'atr_h':            # G_q = Hprev^T R_q, 4 gates
         return 2.0 * B * T * H * 4 * H, f4 * (B * T * H + 4 * n)

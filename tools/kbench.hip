@@ -83,9 +83,33 @@ int main(int argc, char** argv) {
   timeit("atr (R materialised)", f4 * (4 * n + BT * g.H), 2.0 * BT * g.H * 4 * g.H,
          [&] { launch_atr(g, 1, x, S.p[5], R, slab, ns, s); });
   timeit("qgemm side1", f4 * (4 * n + BT * g.H), 2.0 * BT * g.H * 4 * g.H, [&] { launch_qgemm(g, 1, x, S.p[5], G, Q, s); });
-  SweepT sw{x, S, L, zc};
+  SweepT sw{x, S, L, zc, 0, g.B};
   timeit("sweep_t (t=5)", f4 * g.B * (g.D + 27.0 * g.H), 2.0 * g.B * (g.D + g.H) * 4 * g.H,
          [&] { launch_sweep_t(g, 5, w, hp, sw, s); });
+  {
+    hipStream_t s2;
+    hipEvent_t ef, ej;
+    (void)hipStreamCreateWithFlags(&s2, hipStreamNonBlocking);
+    (void)hipEventCreateWithFlags(&ef, hipEventDisableTiming);
+    (void)hipEventCreateWithFlags(&ej, hipEventDisableTiming);
+    const double sb = f4 * g.T * g.B * (g.D + 27.0 * g.H), sf = 2.0 * g.T * g.B * (g.D + g.H) * 4 * g.H;
+    timeit("sweep T steps, 1 stream", sb, sf, [&] {
+      for (int t = 1; t <= g.T; ++t) launch_sweep_t(g, t, w, hp, sw, s);
+    });
+    timeit("sweep T steps, 2 streams", sb, sf, [&] {
+      const int64_t mid = (g.B / 2 + 127) / 128 * 128;
+      (void)hipEventRecord(ef, s);
+      (void)hipStreamWaitEvent(s2, ef, 0);
+      SweepT a1 = sw, a2 = sw;
+      a1.r1 = mid; a2.r0 = mid;
+      for (int t = 1; t <= g.T; ++t) {
+        launch_sweep_t(g, t, w, hp, a1, s);
+        launch_sweep_t(g, t, w, hp, a2, s2);
+      }
+      (void)hipEventRecord(ej, s2);
+      (void)hipStreamWaitEvent(s, ej, 0);
+    });
+  }
   timeit("zgemm", f4 * (4 * n + BT * (g.D + g.H)), 2.0 * BT * (g.D + g.H) * 4 * g.H, [&] { launch_zgemm(g, w, x, S.p[5], zc, s); });
   return 0;
 }

@@ -57,6 +57,8 @@ int dalloc(T** p, size_t n) {
 
 }  // namespace
 
+constexpr int kMaxSweepStreams = 4;
+
 struct AdmmCtx {
   Geom g{};
   Hyper hp{};
@@ -72,9 +74,9 @@ struct AdmmCtx {
   int nblk_resid = 1, nblk_trial = 1, nblk_rx = 1;
   int* found = nullptr;
   int* pick = nullptr;
-  int sweep_split = 1;     // sweep halves on two streams (ADMM_SWEEP_SPLIT=0: one stream)
-  hipStream_t s2 = nullptr;
-  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+  int sweep_split = 2;     // sample parts of the sweep, one stream each (ADMM_SWEEP_SPLIT)
+  hipStream_t sx[kMaxSweepStreams - 1] = {};
+  hipEvent_t ev_fork = nullptr, ev_join[kMaxSweepStreams - 1] = {};
   float *U = nullptr, *wy_slab = nullptr, *Gy = nullptr;
   int wy_nsplit = 1;
   double *ht_part = nullptr, *ht_sums = nullptr;
@@ -260,24 +262,26 @@ int stage_sweep(AdmmCtx* c, hipStream_t s) {
     // per-t kernels concurrently, so one half's HBM-bound epilogue overlaps the other's
     // MFMA-bound GEMM on the same CUs (one kernel per t alone runs them back to back).
     ProfScope ps(c, ADMM_PROF_SWEEP, s);
-    const int64_t mid = c->sweep_split ? std::min<int64_t>((g.B / 2 + 127) / 128 * 128, g.B) : g.B;
-    if (mid < g.B) {
+    // part p of np: rows [p*chunk, (p+1)*chunk), chunk a multiple of the 128-row tile
+    const int np = std::max(1, std::min<int>(c->sweep_split, (int)((g.B + 127) / 128)));
+    const int64_t chunk = ((g.B + np - 1) / np + 127) / 128 * 128;
+    const int nparts = (int)((g.B + chunk - 1) / chunk);
+    hipStream_t st[kMaxSweepStreams];
+    st[0] = s;
+    for (int p = 1; p < nparts; ++p) st[p] = c->sx[p - 1];
+    if (nparts > 1) {
       HIP_TRY(hipEventRecord(c->ev_fork, s));
-      HIP_TRY(hipStreamWaitEvent(c->s2, c->ev_fork, 0));
+      for (int p = 1; p < nparts; ++p) HIP_TRY(hipStreamWaitEvent(st[p], c->ev_fork, 0));
     }
-    for (int t = 1; t <= g.T; ++t) {
-      sa.r0 = 0;
-      sa.r1 = mid;
-      launch_sweep_t(g, t, w, c->hp, sa, s);
-      if (mid < g.B) {
-        sa.r0 = mid;
-        sa.r1 = g.B;
-        launch_sweep_t(g, t, w, c->hp, sa, c->s2);
+    for (int t = 1; t <= g.T; ++t)
+      for (int p = 0; p < nparts; ++p) {
+        sa.r0 = p * chunk;
+        sa.r1 = std::min<int64_t>(sa.r0 + chunk, g.B);
+        launch_sweep_t(g, t, w, c->hp, sa, st[p]);
       }
-    }
-    if (mid < g.B) {
-      HIP_TRY(hipEventRecord(c->ev_join, c->s2));
-      HIP_TRY(hipStreamWaitEvent(s, c->ev_join, 0));
+    for (int p = 1; p < nparts; ++p) {
+      HIP_TRY(hipEventRecord(c->ev_join[p - 1], st[p]));
+      HIP_TRY(hipStreamWaitEvent(s, c->ev_join[p - 1], 0));
     }
   }
   ProfScope ps(c, ADMM_PROF_SMALL, s);
@@ -334,7 +338,8 @@ int admm_create(const AdmmDims* dims, const AdmmParams* params, int device, Admm
   g.H = dims->hidden_size;
   g.O = dims->output_size;
   g.set_T();
-  if (const char* e = std::getenv("ADMM_SWEEP_SPLIT")) c->sweep_split = std::atoi(e) != 0;
+  if (const char* e = std::getenv("ADMM_SWEEP_SPLIT"))
+    c->sweep_split = std::max(1, std::min(kMaxSweepStreams, std::atoi(e)));
   Hyper& h = c->hp;
   for (int i = 0; i < 7; ++i) h.rho[i] = params->rho[i];
   for (int q = 0; q < 4; ++q) {
@@ -369,9 +374,11 @@ int admm_create(const AdmmDims* dims, const AdmmParams* params, int device, Admm
     admm_destroy(c);
     return fail(rc, "%s", msg.c_str());
   }
-  if (hipStreamCreateWithFlags(&c->s2, hipStreamNonBlocking) != hipSuccess ||
-      hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming) != hipSuccess) {
+  bool ok = hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) == hipSuccess;
+  for (int p = 0; ok && p < kMaxSweepStreams - 1; ++p)
+    ok = hipStreamCreateWithFlags(&c->sx[p], hipStreamNonBlocking) == hipSuccess &&
+         hipEventCreateWithFlags(&c->ev_join[p], hipEventDisableTiming) == hipSuccess;
+  if (!ok) {
     admm_destroy(c);
     return fail(ADMM_EHIP, "stream/event creation failed");
   }
@@ -393,8 +400,10 @@ int admm_destroy(AdmmCtx* c) {
   if (c->comm) ncclCommDestroy(c->comm);
   for (hipEvent_t e : c->ev_pool) (void)hipEventDestroy(e);
   if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
-  if (c->ev_join) (void)hipEventDestroy(c->ev_join);
-  if (c->s2) (void)hipStreamDestroy(c->s2);
+  for (int p = 0; p < kMaxSweepStreams - 1; ++p) {
+    if (c->ev_join[p]) (void)hipEventDestroy(c->ev_join[p]);
+    if (c->sx[p]) (void)hipStreamDestroy(c->sx[p]);
+  }
   for (auto& u : c->ev_used) {
     (void)hipEventDestroy(u.second.first);
     (void)hipEventDestroy(u.second.second);

@@ -98,7 +98,13 @@ def pmc_traffic(cls: str, cfg_name: str):
     # trial passes after the first return early (gates already decided): use the full pass
     key = 'traffic_bytes_max' if cls == 'trial' else 'traffic_bytes_median'
     vals = [v[key] for k, v in kern.items() if k.startswith(CLASS_KERNELS[cls])]
-    return sum(vals) / len(vals) if vals else None
+    if not vals:
+        return None
+    per = sum(vals) / len(vals)
+    if cls == 'sweep':   # one class launch = T time steps x 2 sample halves
+        _, T = CONFIGS[cfg_name][0], CONFIGS[cfg_name][1]
+        per *= 2 * T
+    return per
 
 
 def cpu_baseline(cfg_name: str, seconds_hint: float = 20.0):

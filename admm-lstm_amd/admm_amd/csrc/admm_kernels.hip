@@ -624,16 +624,11 @@ __device__ __forceinline__ float expm1_acc(float x) {
 // (relative error grows < 1 ulp per step).  Where -e > 20, m = exp(-e) to 2e-9 and
 // y = exp(-e - w) is taken directly instead (E may underflow while y does not); y is capped
 // at 1e30, where y / (1 + E + y) = 1 (the saturated limit D = -sg sigma(w)).
-template <bool TANH>
-__device__ __forceinline__ void trial_direct(float z, float w, float E, float r, float d0, float qv, int pass,
-                                             float (&acc)[kSlots]) {
+__device__ __forceinline__ void direct_candidates(float cr, float e, float E, float w, float d2,
+                                                  float (&acc)[kSlots]) {
   constexpr float kCap = 1e30f;
-  const float sg = z >= 0.f ? 1.f : -1.f;
-  const float f2 = TANH ? 2.f : 1.f;
-  const float cr = -(f2 * sg) * r;
-  float e = (f2 * sg) * qv * ldexpf(1.f, -(pass * kTrialJ + kTrialJ - 1));   // smallest candidate
   float m = fminf(expm1_acc(-e), kCap);
-  const float one_e = 1.f + E, d2 = 2.f * d0;
+  const float one_e = 1.f + E;
   if (fabsf(e) * (float)(1 << (kTrialJ - 1)) <= 20.f) {   // |e| <= 20 on every candidate: no exp
 #pragma unroll
     for (int k = kTrialJ - 1; k >= 0; --k) {
@@ -655,44 +650,110 @@ __device__ __forceinline__ void trial_direct(float z, float w, float E, float r,
   }
 }
 
-template <bool TANH>
-__device__ __forceinline__ void trial_accumulate(float z, float tg, float qv, int pass, float (&acc)[kSlots]) {
-  // E = exp(-w), r = sigma(w), sc = 1 - sigma(w) on w = |z| (sigmoid) or 2|z| (tanh)
-  const float w = TANH ? 2.f * fabsf(z) : fabsf(z);
-  const float E = expf(-w);
-  const float r = 1.f / (1.f + E);
-  const float sc = E * r;
-  float d0, c1, c2, c3;
-  if (TANH) {
-    const float mz = 2.f * sc;                    // 1 - |tanh z|
-    const float u = copysignf(1.f - mz, z);
-    c1 = mz * (2.f - mz);                         // 1 - u^2
-    c2 = -u * c1;
-    c3 = c1 * (u * u - (1.f / 3.f));
-    d0 = tanhf(z) - tg;                           // the tanh of the stored gate / residual
-  } else {
-    const float s = z >= 0.f ? r : sc, s_c = z >= 0.f ? sc : r;   // = sig_pair(z)
-    const float p = s * s_c;
-    c1 = p;
-    c2 = 0.5f * p * (s_c - s);
-    c3 = p * (1.f - 6.f * p) * (1.f / 6.f);
-    d0 = s - tg;
+// Per-wave queue of the elements in the per-candidate regime.  Which elements need the
+// 16-candidate loop is data dependent (on C3, 0-95 % per gate), so evaluating it in place
+// would run the loop for the whole wave whenever any lane needs it.  Instead each element's
+// five inputs are appended (ballot + prefix count) to an LDS ring of this wave, and the
+// loop runs once 64 entries are pending, with every lane busy.  All lanes of a wave must
+// make the same sequence of dq_push / dq_run calls (loops below are wave-uniform).
+constexpr int kDQ = 128;   // ring capacity: pending <= 63 before a push of <= 64
+struct DirectQ {
+  float* buf;              // this wave's [5][kDQ] in LDS
+  int head, tail;          // wave-uniform counters
+};
+
+__device__ __forceinline__ void dq_push(DirectQ& dq, bool p, float cr, float e, float E, float w, float d2) {
+  const unsigned long long m = __ballot(p);
+  if (p) {
+    const int lane = threadIdx.x & 63;
+    const int slot = (dq.tail + __popcll(m & ((1ull << lane) - 1ull))) & (kDQ - 1);
+    dq.buf[slot] = cr;
+    dq.buf[kDQ + slot] = e;
+    dq.buf[2 * kDQ + slot] = E;
+    dq.buf[3 * kDQ + slot] = w;
+    dq.buf[4 * kDQ + slot] = d2;
   }
-  acc[kSlotFw] += d0 * d0;
-  if (fabsf(qv) <= 0x1p-8f) {
-    if (pass == 0) {
-      const float a1 = c1 * qv, a2 = c2 * qv * qv, a3 = c3 * qv * qv * qv, t = 2.f * d0;
-      acc[kSlotPoly + 0] += t * a1;
-      acc[kSlotPoly + 1] += t * a2 + a1 * a1;
-      acc[kSlotPoly + 2] += t * a3 + 2.f * a1 * a2;
-      acc[kSlotPoly + 3] += a2 * a2 + 2.f * a1 * a3;
-      acc[kSlotPoly + 4] += 2.f * a2 * a3;
-      acc[kSlotPoly + 5] += a3 * a3;
+  dq.tail += __popcll(m);
+}
+
+__device__ __forceinline__ void dq_run(DirectQ& dq, float (&acc)[kSlots], bool final) {
+  while (dq.tail - dq.head >= 64 || (final && dq.tail > dq.head)) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const int lane = threadIdx.x & 63;
+    const int n = dq.tail - dq.head < 64 ? dq.tail - dq.head : 64;
+    if (lane < n) {
+      const int slot = (dq.head + lane) & (kDQ - 1);
+      direct_candidates(dq.buf[slot], dq.buf[kDQ + slot], dq.buf[2 * kDQ + slot], dq.buf[3 * kDQ + slot],
+                        dq.buf[4 * kDQ + slot], acc);
     }
-    return;
+    dq.head += n;
   }
-  acc[kSlotNne] += 1.f;
-  trial_direct<TANH>(z, w, E, r, d0, qv, pass, acc);
+}
+
+// One element of a trial pass: f(W) and polynomial terms in place; per-candidate elements
+// (|q| > 2^-8) go to the wave's queue.  valid = false: no contribution (still pushes).
+//
+// Per-candidate form.  With w = |z| (sigmoid) and sg = sign z,
+// sigma(z + d) - sigma(z) = sg [sigma(w + e) - sigma(w)], e = sg d, and with E = exp(-w),
+// m = expm1(-e), y = E m:
+//   sigma(w + e) - sigma(w) = -sigma(w) y / (1 + E + y)
+// (no cancellation: m carries the difference).  tanh x = 2 sigma(2x) - 1 gives the tanh gate
+// with w = 2|z|, e = 2 sg d and a factor 2.  Along the window d halves, so
+// m_k = m_{k+1} (m_{k+1} + 2): one expm1 for the smallest d, then a multiply per candidate
+// (relative error grows < 1 ulp per step).  Where -e > 20, m = exp(-e) to 2e-9 and
+// y = exp(-e - w) is taken directly instead (E may underflow while y does not); y is capped
+// at 1e30, where y / (1 + E + y) = 1 (the saturated limit D = -sg sigma(w)).
+template <bool TANH>
+__device__ __forceinline__ void trial_point(bool valid, float z, float tg, float qv, int pass, float (&acc)[kSlots],
+                                            DirectQ& dq) {
+  bool direct = false;
+  float cr = 0.f, e = 0.f, E = 0.f, w = 0.f, d2 = 0.f;
+  if (valid) {
+    // E = exp(-w), r = sigma(w), sc = 1 - sigma(w) on w = |z| (sigmoid) or 2|z| (tanh)
+    w = TANH ? 2.f * fabsf(z) : fabsf(z);
+    E = expf(-w);
+    const float r = 1.f / (1.f + E);
+    const float sc = E * r;
+    float d0, c1, c2, c3;
+    if (TANH) {
+      const float mz = 2.f * sc;                    // 1 - |tanh z|
+      const float u = copysignf(1.f - mz, z);
+      c1 = mz * (2.f - mz);                         // 1 - u^2
+      c2 = -u * c1;
+      c3 = c1 * (u * u - (1.f / 3.f));
+      d0 = tanhf(z) - tg;                           // the tanh of the stored gate / residual
+    } else {
+      const float s = z >= 0.f ? r : sc, s_c = z >= 0.f ? sc : r;   // = sig_pair(z)
+      const float p = s * s_c;
+      c1 = p;
+      c2 = 0.5f * p * (s_c - s);
+      c3 = p * (1.f - 6.f * p) * (1.f / 6.f);
+      d0 = s - tg;
+    }
+    acc[kSlotFw] += d0 * d0;
+    if (fabsf(qv) <= 0x1p-8f) {
+      if (pass == 0) {
+        const float a1 = c1 * qv, a2 = c2 * qv * qv, a3 = c3 * qv * qv * qv, t = 2.f * d0;
+        acc[kSlotPoly + 0] += t * a1;
+        acc[kSlotPoly + 1] += t * a2 + a1 * a1;
+        acc[kSlotPoly + 2] += t * a3 + 2.f * a1 * a2;
+        acc[kSlotPoly + 3] += a2 * a2 + 2.f * a1 * a3;
+        acc[kSlotPoly + 4] += 2.f * a2 * a3;
+        acc[kSlotPoly + 5] += a3 * a3;
+      }
+    } else {
+      direct = true;
+      acc[kSlotNne] += 1.f;
+      const float sg = z >= 0.f ? 1.f : -1.f;
+      const float f2 = TANH ? 2.f : 1.f;
+      cr = -(f2 * sg) * r;
+      e = (f2 * sg) * qv * ldexpf(1.f, -(pass * kTrialJ + kTrialJ - 1));   // smallest candidate
+      d2 = 2.f * d0;
+    }
+  }
+  dq_push(dq, direct, cr, e, E, w, d2);
 }
 
 __device__ __forceinline__ void trial_block_store(float (&acc)[kSlots], double* part, int q, int blk, int nblk) {
@@ -710,28 +771,36 @@ __device__ __forceinline__ void trial_block_store(float (&acc)[kSlots], double* 
   }
 }
 
-// Generic trial pass: materialised z (zc) and Q.
+// Generic trial pass: materialised z (zc) and Q.  The loop is wave-uniform (see DirectQ).
 template <bool TANH, int VEC>
 __device__ __forceinline__ void trial_loop(int64_t n, const float* zq, const float* tq, const float* Qq, int pass,
-                                           int blk, int nblk, float (&acc)[kSlots]) {
+                                           int blk, int nblk, float (&acc)[kSlots], DirectQ& dq) {
   const int64_t nv = n / VEC;
   const int64_t stride = (int64_t)nblk * kThreads;
-  for (int64_t v = (int64_t)blk * kThreads + threadIdx.x; v < nv; v += stride) {
+  for (int64_t base = (int64_t)blk * kThreads; base < nv; base += stride) {
+    const int64_t v = base + threadIdx.x;
+    const bool ok = v < nv;
     if (VEC == 4) {
-      const float4 z4 = reinterpret_cast<const float4*>(zq)[v];
-      const float4 t4 = reinterpret_cast<const float4*>(tq)[v];
-      const float4 q4 = reinterpret_cast<const float4*>(Qq)[v];
+      float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f), t4 = z4, q4 = z4;
+      if (ok) {
+        z4 = reinterpret_cast<const float4*>(zq)[v];
+        t4 = reinterpret_cast<const float4*>(tq)[v];
+        q4 = reinterpret_cast<const float4*>(Qq)[v];
+      }
 #pragma unroll 1
       for (int u = 0; u < 4; ++u) {
         const float zu = u == 0 ? z4.x : (u == 1 ? z4.y : (u == 2 ? z4.z : z4.w));
         const float tu = u == 0 ? t4.x : (u == 1 ? t4.y : (u == 2 ? t4.z : t4.w));
         const float qu = u == 0 ? q4.x : (u == 1 ? q4.y : (u == 2 ? q4.z : q4.w));
-        trial_accumulate<TANH>(zu, tu, qu, pass, acc);
+        trial_point<TANH>(ok, zu, tu, qu, pass, acc, dq);
+        dq_run(dq, acc, false);
       }
     } else {
-      trial_accumulate<TANH>(zq[v], tq[v], Qq[v], pass, acc);
+      trial_point<TANH>(ok, ok ? zq[v] : 0.f, ok ? tq[v] : 0.f, ok ? Qq[v] : 0.f, pass, acc, dq);
+      dq_run(dq, acc, false);
     }
   }
+  dq_run(dq, acc, true);
 }
 
 __global__ __launch_bounds__(kThreads) void k_trial(Geom g, int pass, const float* zc, const float* tgt,
@@ -745,13 +814,15 @@ __global__ __launch_bounds__(kThreads) void k_trial(Geom g, int pass, const floa
   float acc[kSlots];
 #pragma unroll
   for (int k = 0; k < kSlots; ++k) acc[k] = 0.f;
+  __shared__ float dqbuf[kThreads / 64][5 * kDQ];
+  DirectQ dq{dqbuf[threadIdx.x >> 6], 0, 0};
   const bool vec = (g.H % 4) == 0;
   if (q == 2) {
-    if (vec) trial_loop<true, 4>(n, zq, tq, Qq, pass, blk, nblk, acc);
-    else trial_loop<true, 1>(n, zq, tq, Qq, pass, blk, nblk, acc);
+    if (vec) trial_loop<true, 4>(n, zq, tq, Qq, pass, blk, nblk, acc, dq);
+    else trial_loop<true, 1>(n, zq, tq, Qq, pass, blk, nblk, acc, dq);
   } else {
-    if (vec) trial_loop<false, 4>(n, zq, tq, Qq, pass, blk, nblk, acc);
-    else trial_loop<false, 1>(n, zq, tq, Qq, pass, blk, nblk, acc);
+    if (vec) trial_loop<false, 4>(n, zq, tq, Qq, pass, blk, nblk, acc, dq);
+    else trial_loop<false, 1>(n, zq, tq, Qq, pass, blk, nblk, acc, dq);
   }
   trial_block_store(acc, part, q, blk, nblk);
 }
@@ -820,23 +891,27 @@ template <bool TANH, int SIDE, int DP, bool XV>
 __device__ __forceinline__ void trial_fast_body(const Geom& g, int q, int pass, const float* __restrict__ zc,
                                                 const float* __restrict__ tgt, const float* __restrict__ Q,
                                                 const float* __restrict__ x, const float* Wlds, int blk, int nblk,
-                                                float (&acc)[kSlots]) {
+                                                float (&acc)[kSlots], DirectQ& dq) {
   const int64_t BT = g.BT(), n = BT * g.H;
   const float* __restrict__ zq = zc + (int64_t)q * n;
   const float* __restrict__ tq = tgt + (int64_t)q * n;
   const float* __restrict__ Qq = Q ? Q + (int64_t)q * n : nullptr;
   const float4* __restrict__ wl4 = reinterpret_cast<const float4*>(Wlds);
   RowCols rc(g.H);
-  if (rc.rr >= rc.rpb) return;
+  const bool lane_ok = rc.rr < rc.rpb;     // idle lanes stay in the (wave-uniform) loop
   const int j = 4 * rc.c4, H4 = g.H / 4;   // fast path: H/4 <= 256, one float4 column per thread
   const int64_t stride = (int64_t)nblk * rc.rpb;
-  for (int64_t row0 = (int64_t)blk * rc.rpb + rc.rr; row0 < BT; row0 += kRPI * stride) {
+  for (int64_t base = (int64_t)blk * rc.rpb; base < BT; base += kRPI * stride) {
+    const int64_t row0 = base + rc.rr;
     float4 z4[kRPI], t4[kRPI], q4[kRPI];
     float xr[kRPI][DP];
+    bool ok[kRPI];
 #pragma unroll
     for (int r = 0; r < kRPI; ++r) {
       const int64_t row = row0 + r * stride;
-      if (row < BT) {
+      ok[r] = lane_ok && row < BT;
+      z4[r] = t4[r] = q4[r] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (ok[r]) {
         z4[r] = *reinterpret_cast<const float4*>(zq + row * g.H + j);
         t4[r] = *reinterpret_cast<const float4*>(tq + row * g.H + j);
         if (SIDE == 0) load_xrow<DP, XV>(x, row, g.D, xr[r]);
@@ -845,17 +920,18 @@ __device__ __forceinline__ void trial_fast_body(const Geom& g, int q, int pass, 
     }
 #pragma unroll
     for (int r = 0; r < kRPI; ++r) {
-      if (row0 + r * stride >= BT) break;
-      if (SIDE == 0) q4[r] = xw_row<DP>(xr[r], wl4, H4, rc.c4);
+      if (SIDE == 0 && ok[r]) q4[r] = xw_row<DP>(xr[r], wl4, H4, rc.c4);
 #pragma unroll 1
       for (int u = 0; u < 4; ++u) {
         const float zu = u == 0 ? z4[r].x : (u == 1 ? z4[r].y : (u == 2 ? z4[r].z : z4[r].w));
         const float tu = u == 0 ? t4[r].x : (u == 1 ? t4[r].y : (u == 2 ? t4[r].z : t4[r].w));
         const float qu = u == 0 ? q4[r].x : (u == 1 ? q4[r].y : (u == 2 ? q4[r].z : q4[r].w));
-        trial_accumulate<TANH>(zu, tu, qu, pass, acc);
+        trial_point<TANH>(ok[r], zu, tu, qu, pass, acc, dq);
+        dq_run(dq, acc, false);
       }
     }
   }
+  dq_run(dq, acc, true);
 }
 
 // Wsrc: side 0 -> G_x [4][D][H]; side 1 -> unused (Q holds the h-side direction)
@@ -870,8 +946,10 @@ __global__ __launch_bounds__(kThreads) void k_trial_fast(Geom g, int pass, const
   float acc[kSlots];
 #pragma unroll
   for (int k = 0; k < kSlots; ++k) acc[k] = 0.f;
-  if (q == 2) trial_fast_body<true, SIDE, DP, XV>(g, q, pass, zc, tgt, Q, x, wlds, blk, nblk, acc);
-  else trial_fast_body<false, SIDE, DP, XV>(g, q, pass, zc, tgt, Q, x, wlds, blk, nblk, acc);
+  __shared__ float dqbuf[kThreads / 64][5 * kDQ];
+  DirectQ dq{dqbuf[threadIdx.x >> 6], 0, 0};
+  if (q == 2) trial_fast_body<true, SIDE, DP, XV>(g, q, pass, zc, tgt, Q, x, wlds, blk, nblk, acc, dq);
+  else trial_fast_body<false, SIDE, DP, XV>(g, q, pass, zc, tgt, Q, x, wlds, blk, nblk, acc, dq);
   trial_block_store(acc, part, q, blk, nblk);
 }
 
@@ -995,14 +1073,16 @@ __global__ __launch_bounds__(kThreads) void k_trial_debug(int64_t n, int tanh_ga
   for (int k = 0; k < kSlots; ++k) acc[k] = 0.f;
   const int pass = kbase / kTrialJ;
   // the polynomial slots are only filled on pass 0: run pass 0 for them, then this pass
-  if (tanh_gate) trial_loop<true, 1>(n, z, tgt, qv, 0, blockIdx.x, gridDim.x, acc);
-  else trial_loop<false, 1>(n, z, tgt, qv, 0, blockIdx.x, gridDim.x, acc);
+  __shared__ float dqbuf[kThreads / 64][5 * kDQ];
+  DirectQ dq{dqbuf[threadIdx.x >> 6], 0, 0};
+  if (tanh_gate) trial_loop<true, 1>(n, z, tgt, qv, 0, blockIdx.x, gridDim.x, acc, dq);
+  else trial_loop<false, 1>(n, z, tgt, qv, 0, blockIdx.x, gridDim.x, acc, dq);
   if (pass > 0) {
     float acc2[kSlots];
 #pragma unroll
     for (int k = 0; k < kSlots; ++k) acc2[k] = 0.f;
-    if (tanh_gate) trial_loop<true, 1>(n, z, tgt, qv, pass, blockIdx.x, gridDim.x, acc2);
-    else trial_loop<false, 1>(n, z, tgt, qv, pass, blockIdx.x, gridDim.x, acc2);
+    if (tanh_gate) trial_loop<true, 1>(n, z, tgt, qv, pass, blockIdx.x, gridDim.x, acc2, dq);
+    else trial_loop<false, 1>(n, z, tgt, qv, pass, blockIdx.x, gridDim.x, acc2, dq);
 #pragma unroll
     for (int k = 0; k < kTrialJ; ++k) acc[k] = acc2[k];
   }

@@ -900,6 +900,7 @@ __device__ __forceinline__ void trial_fast_body(const Geom& g, int q, int pass, 
   RowCols rc(g.H);
   const bool lane_ok = rc.rr < rc.rpb;     // idle lanes stay in the (wave-uniform) loop
   const int j = 4 * rc.c4, H4 = g.H / 4;   // fast path: H/4 <= 256, one float4 column per thread
+  constexpr int kRPI = SIDE == 0 ? 1 : 2;   // side 0 keeps its x rows live: one row per pass
   const int64_t stride = (int64_t)nblk * rc.rpb;
   for (int64_t base = (int64_t)blk * rc.rpb; base < BT; base += kRPI * stride) {
     const int64_t row0 = base + rc.rr;
@@ -911,6 +912,10 @@ __device__ __forceinline__ void trial_fast_body(const Geom& g, int q, int pass, 
       const int64_t row = row0 + r * stride;
       ok[r] = lane_ok && row < BT;
       z4[r] = t4[r] = q4[r] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (SIDE == 0) {
+#pragma unroll
+        for (int d = 0; d < DP; ++d) xr[r][d] = 0.f;
+      }
       if (ok[r]) {
         z4[r] = *reinterpret_cast<const float4*>(zq + row * g.H + j);
         t4[r] = *reinterpret_cast<const float4*>(tq + row * g.H + j);
@@ -918,9 +923,19 @@ __device__ __forceinline__ void trial_fast_body(const Geom& g, int q, int pass, 
         else q4[r] = *reinterpret_cast<const float4*>(Qq + row * g.H + j);
       }
     }
+    if (SIDE == 0) {   // q = x_row . G_x for both rows, one LDS read of G_x per d
+#pragma unroll
+      for (int d = 0; d < DP; ++d) {
+        const float4 wv = wl4[d * H4 + rc.c4];
+#pragma unroll
+        for (int r = 0; r < kRPI; ++r) {
+          q4[r].x = fmaf(xr[r][d], wv.x, q4[r].x); q4[r].y = fmaf(xr[r][d], wv.y, q4[r].y);
+          q4[r].z = fmaf(xr[r][d], wv.z, q4[r].z); q4[r].w = fmaf(xr[r][d], wv.w, q4[r].w);
+        }
+      }
+    }
 #pragma unroll
     for (int r = 0; r < kRPI; ++r) {
-      if (SIDE == 0 && ok[r]) q4[r] = xw_row<DP>(xr[r], wl4, H4, rc.c4);
 #pragma unroll 1
       for (int u = 0; u < 4; ++u) {
         const float zu = u == 0 ? z4[r].x : (u == 1 ? z4[r].y : (u == 2 ? z4[r].z : z4[r].w));

@@ -38,6 +38,40 @@ __device__ __forceinline__ float sigm(float z) { return sig_pair(z).s; }
 
 __device__ __forceinline__ float act(bool is_tanh, float z) { return is_tanh ? tanhf(z) : sigm(z); }
 
+// expm1(x) to ~1 ulp: degree-8 Taylor on |x| < 1/2 (truncation < 2^-26 relative), else exp - 1
+__device__ __forceinline__ float expm1_acc(float x) {
+  if (fabsf(x) < 0.5f) {
+    float p = 1.f / 40320.f;
+    p = fmaf(p, x, 1.f / 5040.f);
+    p = fmaf(p, x, 1.f / 720.f);
+    p = fmaf(p, x, 1.f / 120.f);
+    p = fmaf(p, x, 1.f / 24.f);
+    p = fmaf(p, x, 1.f / 6.f);
+    p = fmaf(p, x, 0.5f);
+    p = fmaf(p, x, 1.f);
+    return p * x;
+  }
+  return __expf(x) - 1.f;
+}
+
+// phi(z) and phi'(z) for the gradient / residual / line-search paths, from one v_exp and one
+// v_rcp (a few ulp; these feed sums, not the stored state).  With w = |z| (sigmoid) or 2|z|
+// (tanh), E = exp(-w), r = 1/(1+E):  sigma: phi = r or E r, phi' = E r^2;  tanh: |phi| =
+// -expm1(-w) r (no cancellation near 0), phi' = 4 E r^2.
+template <bool TANH>
+__device__ __forceinline__ void phi_fast(float z, float& phi, float& dphi) {
+  const float w = TANH ? 2.f * fabsf(z) : fabsf(z);
+  const float E = __expf(-w);
+  const float r = __builtin_amdgcn_rcpf(1.f + E);
+  if (TANH) {
+    phi = copysignf(-expm1_acc(-w) * r, z);
+    dphi = 4.f * E * r * r;
+  } else {
+    phi = z >= 0.f ? r : E * r;
+    dphi = E * r * r;
+  }
+}
+
 // ----------------------------------------------------------------------------- reductions
 
 __device__ __forceinline__ float wave_sum(float v) {

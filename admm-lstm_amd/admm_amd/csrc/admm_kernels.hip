@@ -449,14 +449,7 @@ struct AtRFusedSrc {
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       float phi, dphi;
-      if (TANH) {
-        phi = tanhf(zz[u]);
-        dphi = 1.f - phi * phi;
-      } else {
-        const SigPair sp = sig_pair(zz[u]);
-        phi = sp.s;
-        dphi = sp.s * sp.sc;
-      }
+      phi_fast<TANH>(zz[u], phi, dphi);
       r[u] = (phi - tt[u]) * dphi;
     }
     return make_float4(r[0], r[1], r[2], r[3]);
@@ -598,32 +591,6 @@ __global__ __launch_bounds__(kThreads) void k_qgemm(Geom g, const float* x, cons
 constexpr int kSlots = kTrialSlots;
 constexpr int kSlotPoly = kTrialJ, kSlotFw = kTrialJ + kPolyN, kSlotNne = kTrialJ + kPolyN + 1;
 
-// expm1(x) to ~1 ulp: degree-8 Taylor on |x| < 1/2 (truncation < 2^-26 relative), else exp - 1
-__device__ __forceinline__ float expm1_acc(float x) {
-  if (fabsf(x) < 0.5f) {
-    float p = 1.f / 40320.f;
-    p = fmaf(p, x, 1.f / 5040.f);
-    p = fmaf(p, x, 1.f / 720.f);
-    p = fmaf(p, x, 1.f / 120.f);
-    p = fmaf(p, x, 1.f / 24.f);
-    p = fmaf(p, x, 1.f / 6.f);
-    p = fmaf(p, x, 0.5f);
-    p = fmaf(p, x, 1.f);
-    return p * x;
-  }
-  return __expf(x) - 1.f;
-}
-
-// Per-candidate increments of one element, all J candidates of the window, no branches.
-// With w = |z| (sigmoid) and sg = sign z, sigma(z + d) - sigma(z) = sg [sigma(w + e) - sigma(w)],
-// e = sg d, and with E = exp(-w), m = expm1(-e), y = E m:
-//   sigma(w + e) - sigma(w) = -sigma(w) y / (1 + E + y)
-// (no cancellation: m carries the difference).  tanh x = 2 sigma(2x) - 1 gives the tanh gate
-// with w = 2|z|, e = 2 sg d and a factor 2.  Along the window d halves, so
-// m_k = m_{k+1} (m_{k+1} + 2): one expm1 for the smallest d, then a multiply per candidate
-// (relative error grows < 1 ulp per step).  Where -e > 20, m = exp(-e) to 2e-9 and
-// y = exp(-e - w) is taken directly instead (E may underflow while y does not); y is capped
-// at 1e30, where y / (1 + E + y) = 1 (the saturated limit D = -sg sigma(w)).
 __device__ __forceinline__ void direct_candidates(float cr, float e, float E, float w, float d2,
                                                   float (&acc)[kSlots]) {
   constexpr float kCap = 1e30f;
@@ -713,8 +680,8 @@ __device__ __forceinline__ void trial_point(bool valid, float z, float tg, float
   if (valid) {
     // E = exp(-w), r = sigma(w), sc = 1 - sigma(w) on w = |z| (sigmoid) or 2|z| (tanh)
     w = TANH ? 2.f * fabsf(z) : fabsf(z);
-    E = expf(-w);
-    const float r = 1.f / (1.f + E);
+    E = __expf(-w);
+    const float r = __builtin_amdgcn_rcpf(1.f + E);
     const float sc = E * r;
     float d0, c1, c2, c3;
     if (TANH) {
@@ -723,7 +690,7 @@ __device__ __forceinline__ void trial_point(bool valid, float z, float tg, float
       c1 = mz * (2.f - mz);                         // 1 - u^2
       c2 = -u * c1;
       c3 = c1 * (u * u - (1.f / 3.f));
-      d0 = tanhf(z) - tg;                           // the tanh of the stored gate / residual
+      d0 = copysignf(-expm1_acc(-w) * r, z) - tg;  // tanh z = sg (1 - E) / (1 + E)
     } else {
       const float s = z >= 0.f ? r : sc, s_c = z >= 0.f ? sc : r;   // = sig_pair(z)
       const float p = s * s_c;
@@ -1044,14 +1011,8 @@ __global__ __launch_bounds__(kThreads) void k_resid_gx(Geom g, Hyper hp, const f
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
         float phi, dphi;
-        if (th) {
-          phi = tanhf(zz[u]);
-          dphi = 1.f - phi * phi;
-        } else {
-          const SigPair sp = sig_pair(zz[u]);
-          phi = sp.s;
-          dphi = sp.s * sp.sc;
-        }
+        if (th) phi_fast<true>(zz[u], phi, dphi);
+        else phi_fast<false>(zz[u], phi, dphi);
         const float R = (phi - tt[u]) * dphi;
 #pragma unroll
         for (int d = 0; d < DP; ++d) acc[d][u] += xr[d] * R;

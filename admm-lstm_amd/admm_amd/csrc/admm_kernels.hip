@@ -7,6 +7,8 @@
 //   output weight wy ................ admm.py:246-280, admm.no_dual_y.py:226-249
 //   h_T search, a, duals at T ....... admm.py:459-502, 532-546, admm.no_dual_y.py:414-456
 // Layouts: gates/duals [B][T+1][H] (the reference's), caches [4][B*T][H] (row = b*T + t-1).
+#include <cstdlib>
+
 #include "admm_dev.hpp"
 #include "admm_kernels.hpp"
 
@@ -456,11 +458,11 @@ struct AtRFusedSrc {
   }
 };
 
-template <bool TANH>
+template <int BM, int WM, int KC, bool TANH>
 __device__ __forceinline__ void atr_fused_body(const Geom& g, const float* x, const float* Sh, const float* zc,
                                                const float* tgt, const float* dW, float* slab, int nsplit,
                                                float* smem) {
-  constexpr int BM = 128, BN = 128, WM = 64, WN = 64, KC = 32;
+  constexpr int BN = 128, WN = 64;
   using S = Tile<BM, BN, WM, WN, KC, false>;
   const int nm = (g.H + BM - 1) / BM, nn = (g.H + BN - 1) / BN;
   int lid = xcd_swizzle(blockIdx.x, gridDim.x);
@@ -493,14 +495,17 @@ __device__ __forceinline__ void atr_fused_body(const Geom& g, const float* x, co
     }
 }
 
-constexpr int ATR_FUSED_LDS = Tile<128, 128, 64, 64, 32, false>::LDS_FLOATS;
-
+// Tiles: BM = 128 (2 x 2 waves of 64 x 64, KC = 32) or BM = 256 (the whole hidden dim of the
+// A^T side for H = 256: z and tgt are then streamed once; 2 x 2 waves of 128 x 64, KC = 16).
+template <int BM, int WM, int KC>
 __global__ __launch_bounds__(kThreads) void k_atr_fused(Geom g, const float* x, const float* Sh, const float* zc,
                                                           const float* tgt, const float* dW, float* slab, int nsplit) {
-  __shared__ float smem[ATR_FUSED_LDS];
-  const int nm = (g.H + 127) / 128, nn = (g.H + 127) / 128;
-  if ((xcd_swizzle(blockIdx.x, gridDim.x) / (nm * nn)) % 4 == 2) atr_fused_body<true>(g, x, Sh, zc, tgt, dW, slab, nsplit, smem);
-  else atr_fused_body<false>(g, x, Sh, zc, tgt, dW, slab, nsplit, smem);
+  __shared__ float smem[Tile<BM, 128, WM, 64, KC, false>::LDS_FLOATS];
+  const int nm = (g.H + BM - 1) / BM, nn = (g.H + 127) / 128;
+  if ((xcd_swizzle(blockIdx.x, gridDim.x) / (nm * nn)) % 4 == 2)
+    atr_fused_body<BM, WM, KC, true>(g, x, Sh, zc, tgt, dW, slab, nsplit, smem);
+  else
+    atr_fused_body<BM, WM, KC, false>(g, x, Sh, zc, tgt, dW, slab, nsplit, smem);
 }
 
 __global__ __launch_bounds__(kThreads) void k_reduce_g(int Kd, int H, Hyper hp, const float* slab, int nsplit,
@@ -1455,6 +1460,15 @@ void launch_resid(const Geom& g, const Hyper& hp, const ResidArgs& a, hipStream_
   k_resid<<<grid, kThreads, 0, s>>>(g, hp, a);
 }
 
+static int g_atr_wide = -1;
+bool atr_wide(const Geom& g) {
+  if (g_atr_wide < 0) {
+    const char* e = std::getenv("ADMM_ATR_WIDE");
+    g_atr_wide = e ? std::atoi(e) : 1;
+  }
+  return g_atr_wide && g.H % 256 == 0;
+}
+
 int atr_splits(const Geom& g, int side) {
   const int Kd = side == 0 ? g.D : g.H;
   const int tiles = cdiv64(Kd, side == 1 ? 128 : 32) * cdiv64(g.H, 128) * 4;
@@ -1542,8 +1556,13 @@ void launch_resid_gx(const Geom& g, const Hyper& hp, const float* x, const Plane
 void launch_atr_fused(const Geom& g, const Hyper& hp, const float* x, const float* Sh, const float* zc,
                       const float* tgt, const float* dW, float* slab, int nsplit, hipStream_t s) {
   (void)hp;
-  dim3 grid(cdiv64(g.H, 128) * cdiv64(g.H, 128) * 4 * nsplit);
-  k_atr_fused<<<grid, kThreads, 0, s>>>(g, x, Sh, zc, tgt, dW, slab, nsplit);
+  if (atr_wide(g)) {
+    dim3 grid(cdiv64(g.H, 256) * cdiv64(g.H, 128) * 4 * nsplit);
+    k_atr_fused<256, 128, 16><<<grid, kThreads, 0, s>>>(g, x, Sh, zc, tgt, dW, slab, nsplit);
+  } else {
+    dim3 grid(cdiv64(g.H, 128) * cdiv64(g.H, 128) * 4 * nsplit);
+    k_atr_fused<128, 64, 32><<<grid, kThreads, 0, s>>>(g, x, Sh, zc, tgt, dW, slab, nsplit);
+  }
 }
 
 int stream_blocks(const Geom& g) {   // streaming passes: ~2 rows in flight per thread

@@ -1088,15 +1088,13 @@ __global__ __launch_bounds__(kThreads) void k_trial_debug(int64_t n, int tanh_ga
 __global__ __launch_bounds__(kThreads) void k_trial_reduce(int pass, const double* part, int nblk, const int* found,
                                                              double* sums) {
   __shared__ double red[4];
-  const int q = blockIdx.x;
+  const int k = blockIdx.x, q = blockIdx.y;      // one block per (slot, gate)
   if (found[q]) return;
-  for (int k = 0; k < kSlots; ++k) {
-    double s = 0.0;
-    const double* p = part + ((int64_t)q * kSlots + k) * nblk;
-    for (int i = threadIdx.x; i < nblk; i += kThreads) s += p[i];
-    const double tot = block_sum(s, red);
-    if (threadIdx.x == 0) sums[q * kSlots + k] = tot;
-  }
+  double s = 0.0;
+  const double* p = part + ((int64_t)q * kSlots + k) * nblk;
+  for (int i = threadIdx.x; i < nblk; i += kThreads) s += p[i];
+  const double tot = block_sum(s, red);
+  if (threadIdx.x == 0) sums[q * kSlots + k] = tot;
 }
 
 // First k with f(W + G/2^k) <= est_k (admm.py:331-336); then
@@ -1530,7 +1528,7 @@ void launch_trial_debug(int64_t n, int tanh_gate, int kbase, const float* z, con
 void launch_trial_reduce(const Geom& g, int pass, const double* part, int nblk, const int* found, double* sums,
                          hipStream_t s) {
   (void)g;
-  k_trial_reduce<<<4, kThreads, 0, s>>>(pass, part, nblk, found, sums);
+  k_trial_reduce<<<dim3(kSlots, 4), kThreads, 0, s>>>(pass, part, nblk, found, sums);
 }
 
 bool fast_path(const Geom& g) {

@@ -55,11 +55,29 @@ CASES = {
     # C2 shapes
     't2_c2':        ('admm', False, 'uniform', 2048, 16, 16, 64, 6, False, 'GoogleStock'),
     't2_c2_nd_rw':  ('no_dual_y', False, 'rw', 1024, 16, 1, 64, 6, False, 'GoogleStock'),
+    # C1: the real GoogleStock windows (demo.py defaults: hidden 10, 30 epochs), train + val losses
+    'c1_goog':      ('admm', False, 'goog', 4224, 10, 1, 10, 30, False, 'GoogleStock'),
 }
+
+
+def goog_windows():
+    """C1 inputs: GOOG.xls columns (tests/golden/goog_cols45.npz, extracted by
+    tools/extract_goog.py) through the package's restatement of dataset.py:406-440."""
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(OUT)), 'admm-lstm_amd'))
+    import dataset as ds  # the package's dataset module (GoogleStock only)
+    f = np.load(os.path.join(OUT, 'goog_cols45.npz'))
+    tx, ty, vx, vy = ds.google_stock_windows(f['col_x'].tolist(), f['col_y'].tolist())
+    sys.path.pop(0)
+    sys.modules.pop('dataset', None)
+    return tx.contiguous(), ty.contiguous(), vx.contiguous(), vy.contiguous()
 
 
 def make_inputs(gen: str, B: int, T: int, D: int):
     """Synthetic inputs of SURVEY.md section 8(d)."""
+    if gen == 'goog':
+        tx, ty, _, _ = goog_windows()
+        assert tuple(tx.shape) == (B, T, D)
+        return tx, ty
     if gen == 'uniform':
         g = torch.Generator().manual_seed(1234)
         x = torch.rand(B, T, D, generator=g)
@@ -145,6 +163,15 @@ def run_case(name):
         with torch.no_grad():
             return float(loss_fn(model(x), y))
 
+    vx = vy = None
+    if gen == 'goog':
+        _, _, vx, vy = goog_windows()
+        arrays['val_x'], arrays['val_y'] = vx.numpy(), vy.numpy()
+
+    def val_loss():
+        with torch.no_grad():
+            return float(loss_fn(model(vx), vy)) if vx is not None else None
+
     opt = mod.ADMMBasedOptimizer(model, (x, y), pdict, verbose=False)
 
     def snap_state(prefix):
@@ -157,6 +184,7 @@ def run_case(name):
     if full:
         snap_state('s0')
     losses = [loss()]
+    val_losses = [val_loss()]
     searches, step_times = [], []
     for s in range(1, steps + 1):
         with GtRecorder() as rec:
@@ -180,12 +208,13 @@ def run_case(name):
         if full:
             snap_state(f's{s}')
         losses.append(loss())
+        val_losses.append(val_loss())
         print(f'{name}: step {s} loss {losses[-1]:.8f} k={[len(v) - 1 for v in searches[-1]["weights"]]} '
               f'hT={len(searches[-1]["hT"])} ({step_times[-1]:.2f}s)', flush=True)
     meta = {
         'name': name, 'variant': variant, 'with_dual_y': dual_y, 'gen': gen,
         'B': B, 'T': T, 'D': D, 'H': H, 'O': 1, 'steps': steps, 'full_state': full,
-        'param_set': pset, 'params': pdict, 'losses': losses, 'searches': searches,
+        'param_set': pset, 'params': pdict, 'losses': losses, 'val_losses': val_losses, 'searches': searches,
         'torch': torch.__version__, 'threads': torch.get_num_threads(), 'step_times': step_times,
         'generator': 'tests/golden/make_golden.py',
     }

@@ -48,5 +48,6 @@ class Golden:
         return [len(v) - 1 for v in self.searches[step - 1]['weights']]
 
 
-ALL = sorted(f[:-4] for f in os.listdir(GOLDEN) if f.endswith('.npz'))
+# step fixtures (goog_cols45.npz holds the C1 input columns, not a step trajectory)
+ALL = sorted(f[:-4] for f in os.listdir(GOLDEN) if f.endswith('.npz') and not f.startswith('goog_'))
 FULL = [n for n in ALL if Golden(n).full_state]

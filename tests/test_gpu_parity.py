@@ -83,7 +83,9 @@ def _fp64_step_decisions(g: Golden, W, S, L):
         torch.set_default_dtype(torch.float32)
 
 
-@pytest.mark.parametrize('name', ALL)
+# c1_goog (real data) has noise-level reference decisions after step 15: checked per
+# iteration below instead of as a free-running trajectory
+@pytest.mark.parametrize('name', [n for n in ALL if n != 'c1_goog'])
 def test_trajectory_loss_matches_reference(name, mods, dev):
     g = Golden(name)
     model, opt = _optimizer(g, mods, dev)
@@ -99,6 +101,44 @@ def test_trajectory_loss_matches_reference(name, mods, dev):
             for q in GATES6:
                 assert float((opt.gates[q].cpu() - S[q]).abs().max()) <= STATE_ATOL, (s, q)
                 assert float((opt.duals[q].cpu() - L[q]).abs().max()) <= STATE_ATOL, (s, q)
+
+
+def test_c1_googlestock_trajectory(mods, dev):
+    """C1 (real GoogleStock windows, hidden 10, 30 epochs as demo.py): training AND validation
+    loss per epoch (demo.py:337-356 records both) within 1e-5 relative of the reference's,
+    up to the first epoch where the reference's fp32 line search decides on rounding noise
+    (on this data from about epoch 15).  At that epoch every search the
+    GPU decided differently must carry the fp64 decision taken from the same pre-step state,
+    and the reference must have departed from fp64 in at least one search; the trajectories
+    are different (equally valid) ADMM runs from there on.  (The CPU oracle reproduces the
+    reference's noise only with the reference's CPU summation order, so it cannot serve as
+    the per-step reference on the GPU box.)"""
+    g = Golden('c1_goog')
+    model, opt = _optimizer(g, mods, dev)
+    x, y = g.x.to(dev), g.y.to(dev)
+    vx, vy = g.t('val_x').to(dev), g.t('val_y').to(dev)
+    names = list(opt.last_step_stats()['k'].keys())
+    assert _loss(model, vx, vy) == pytest.approx(g.val_losses[0], rel=LOSS_RTOL)
+    matched = 0
+    for s in range(1, g.steps + 1):
+        W = {k: p.detach().cpu().clone() for k, p in model.named_parameters()}
+        S = {k: v.cpu().clone() for k, v in opt.gates.items()}
+        L = {k: v.cpu().clone() for k, v in opt.duals.items()}
+        opt.step()
+        tr, va = _loss(model, x, y), _loss(model, vx, vy)
+        if tr == pytest.approx(g.losses[s], rel=LOSS_RTOL) and va == pytest.approx(g.val_losses[s], rel=LOSS_RTOL):
+            matched += 1
+            continue
+        ks = [opt.last_step_stats()['k'][n] for n in names]
+        ref_ks = g.ks(s)
+        fp64 = _fp64_step_decisions(g, W, S, L)
+        for i, (a, r) in enumerate(zip(ks, ref_ks)):
+            if a != r:
+                k64, margin = fp64[i]
+                assert a == k64 or (margin < 1e-3 and abs(a - k64) <= 1), (s, i, ks, ref_ks, fp64)
+        assert any(r != k64 for r, (k64, _) in zip(ref_ks, fp64)), (s, ks, ref_ks, fp64)
+        break
+    assert matched >= 10, matched
 
 
 @pytest.mark.parametrize('name', FULL)

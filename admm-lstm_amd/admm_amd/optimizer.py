@@ -273,6 +273,35 @@ class AdmmOptimizerBase(object):
             'direct_frac': {name: s.direct_frac[i] for i, name in enumerate(WEIGHT_ORDER)},
         }
 
+    # ------------------------------------------------------------------ checkpoint
+    def state_dict(self) -> dict:
+        """The primal/dual state (``gates``, ``duals`` incl. ``a`` and dual ``y``) as CPU
+        tensors plus the shape; ``torch.save`` of it loads back with ``weights_only=True``.
+        With the model's own ``state_dict`` this is everything a later step depends on (the
+        z cache is rebuilt from them)."""
+        return {
+            'format': 'admm-lstm-mi355x/optimizer-state/1',
+            'shape': [self.batch_size, self.seq_len, self.input_size, self.hidden_size, self.output_size],
+            'gates': {k: v.detach().cpu().clone() for k, v in self.gates.items()},
+            'duals': {k: v.detach().cpu().clone() for k, v in self.duals.items()},
+        }
+
+    def load_state_dict(self, state: dict) -> None:
+        """Copy a ``state_dict()`` into this optimizer's (bound) device tensors."""
+        shape = [self.batch_size, self.seq_len, self.input_size, self.hidden_size, self.output_size]
+        if list(state.get('shape', [])) != shape:
+            raise ValueError(f'checkpoint is for shape {state.get("shape")}, this optimizer has {shape}')
+        with torch.no_grad():
+            for part, dst in (('gates', self.gates), ('duals', self.duals)):
+                src = state[part]
+                if set(src) != set(dst):
+                    raise ValueError(f'checkpoint {part} keys {sorted(src)} != {sorted(dst)}')
+                for k, t in dst.items():
+                    if tuple(src[k].shape) != tuple(t.shape):
+                        raise ValueError(f'checkpoint {part}[{k!r}] has shape {tuple(src[k].shape)}')
+                    t.copy_(src[k].to(t.device, torch.float32))
+        # gates['h'] changed version: the next step() rebuilds the z cache
+
     def profile(self, classes=()) -> None:
         """Enable live hipEvent timing of the named kernel classes (``_native.PROF_CLASSES``)."""
         mask = 0

@@ -141,6 +141,29 @@ def test_c1_googlestock_trajectory(mods, dev):
     assert matched >= 10, matched
 
 
+def test_checkpoint_resume(mods, dev, tmp_path):
+    """3 steps, checkpoint (model + optimizer state), a fresh model/optimizer restored from
+    it, 2 more steps == 5 uninterrupted steps (the restored run rebuilds its z cache)."""
+    from admm_amd.checkpoint import load_checkpoint, save_checkpoint
+    g = Golden('t2_c2')
+    model, opt = _optimizer(g, mods, dev)
+    x, y = g.x.to(dev), g.y.to(dev)
+    for _ in range(3):
+        opt.step()
+    path = str(tmp_path / 'c2.pt')
+    save_checkpoint(path, model, opt)
+    for _ in range(2):
+        opt.step()
+    model2, opt2 = _optimizer(g, mods, dev)               # fresh init, then restore
+    load_checkpoint(path, model2, opt2)
+    for _ in range(2):
+        opt2.step()
+    assert _loss(model2, x, y) == pytest.approx(_loss(model, x, y), rel=LOSS_RTOL)
+    assert _loss(model2, x, y) == pytest.approx(g.losses[5], rel=LOSS_RTOL)
+    for q in GATES6:
+        assert float((opt2.gates[q] - opt.gates[q]).abs().max()) <= STATE_ATOL, q
+
+
 @pytest.mark.parametrize('name', FULL)
 def test_teacher_forced_steps(name, mods, dev):
     """Load the reference state after step k into the optimizer, step once, compare with k+1."""

@@ -17,6 +17,19 @@ namespace admm {
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
+// Streaming (non-temporal) accesses for data touched once per pass: the ADMM state planes,
+// the z cache and the line-search targets.  Calibrated on the box (tools/streambench.hip):
+// +7 % read, +10 % copy bandwidth over plain loads/stores.
+__device__ __forceinline__ float4 ld_nt(const float* p) {
+  const f32x4 v = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(p));
+  return make_float4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ void st_nt(float* p, const float4& v) {
+  __builtin_nontemporal_store(f32x4{v.x, v.y, v.z, v.w}, reinterpret_cast<f32x4*>(p));
+}
+__device__ __forceinline__ float ld_nt(const float* p, int) { return __builtin_nontemporal_load(p); }
+__device__ __forceinline__ void st_nt(float* p, float v) { __builtin_nontemporal_store(v, p); }
+
 constexpr int kWave = 64;
 constexpr int kThreads = 256;  // every kernel: 4 waves per workgroup
 

@@ -889,10 +889,10 @@ __device__ __forceinline__ void trial_fast_body(const Geom& g, int q, int pass, 
         for (int d = 0; d < DP; ++d) xr[r][d] = 0.f;
       }
       if (ok[r]) {
-        z4[r] = *reinterpret_cast<const float4*>(zq + row * g.H + j);
-        t4[r] = *reinterpret_cast<const float4*>(tq + row * g.H + j);
+        z4[r] = ld_nt(zq + row * g.H + j);
+        t4[r] = ld_nt(tq + row * g.H + j);
         if (SIDE == 0) load_xrow<DP, XV>(x, row, g.D, xr[r]);
-        else q4[r] = *reinterpret_cast<const float4*>(Qq + row * g.H + j);
+        else q4[r] = ld_nt(Qq + row * g.H + j);
       }
     }
     if (SIDE == 0) {   // q = x_row . G_x for both rows, one LDS read of G_x per d
@@ -962,7 +962,7 @@ __global__ __launch_bounds__(kThreads) void k_apply_dwx(Geom g, const float* __r
     for (int r = 0; r < kRPI; ++r) {
       const int64_t row = row0 + r * stride;
       if (row < BT) {
-        z4[r] = *reinterpret_cast<const float4*>(zq + row * g.H + j);
+        z4[r] = ld_nt(zq + row * g.H + j);
         load_xrow<DP, XV>(x, row, g.D, xr[r]);
       }
     }
@@ -973,7 +973,7 @@ __global__ __launch_bounds__(kThreads) void k_apply_dwx(Geom g, const float* __r
       const float4 dz = xw_row<DP>(xr[r], wl4, H4, rc.c4);
       float4 zn;
       zn.x = z4[r].x + dz.x; zn.y = z4[r].y + dz.y; zn.z = z4[r].z + dz.z; zn.w = z4[r].w + dz.w;
-      *reinterpret_cast<float4*>(zq + row * g.H + j) = zn;
+      st_nt(zq + row * g.H + j, zn);
     }
   }
 }
@@ -1006,12 +1006,12 @@ __global__ __launch_bounds__(kThreads) void k_resid_gx(Geom g, Hyper hp, const f
       const int64_t so = (row + b + 1) * g.H;  // (b*(T+1) + t) * H with t = row - b*T + 1
       float xr[DP];
       load_xrow<DP, XV>(x, row, g.D, xr);
-      const float4 z4 = *reinterpret_cast<const float4*>(zq + row * g.H + j);
-      const float4 l4 = *reinterpret_cast<const float4*>(Lq + so + j);
-      const float4 s4 = *reinterpret_cast<const float4*>(Sq + so + j);
+      const float4 z4 = ld_nt(zq + row * g.H + j);
+      const float4 l4 = ld_nt(Lq + so + j);
+      const float4 s4 = ld_nt(Sq + so + j);
       float4 t4;
       t4.x = l4.x / rho + s4.x; t4.y = l4.y / rho + s4.y; t4.z = l4.z / rho + s4.z; t4.w = l4.w / rho + s4.w;
-      *reinterpret_cast<float4*>(tq + row * g.H + j) = t4;
+      st_nt(tq + row * g.H + j, t4);
       const float zz[4] = {z4.x, z4.y, z4.z, z4.w}, tt[4] = {t4.x, t4.y, t4.z, t4.w};
 #pragma unroll
       for (int u = 0; u < 4; ++u) {

@@ -49,6 +49,36 @@ __global__ void k_copy(int64_t n4, const float4* __restrict__ a, float4* __restr
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256) b[i] = a[i];
 }
 
+// read-only stream with a reduction (trial-like): sum of 3 planes
+template <bool NT>
+__global__ __launch_bounds__(256) void k_read3(int64_t n4, const float4* __restrict__ a, const float4* __restrict__ b,
+                                               const float4* __restrict__ c, float* out) {
+  float s = 0.f;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256) {
+    float4 x, y, z;
+    if (NT) {
+      typedef float v4 __attribute__((ext_vector_type(4)));
+      const v4 xa = __builtin_nontemporal_load(reinterpret_cast<const v4*>(a) + i);
+      const v4 ya = __builtin_nontemporal_load(reinterpret_cast<const v4*>(b) + i);
+      const v4 za = __builtin_nontemporal_load(reinterpret_cast<const v4*>(c) + i);
+      x = make_float4(xa.x, xa.y, xa.z, xa.w); y = make_float4(ya.x, ya.y, ya.z, ya.w); z = make_float4(za.x, za.y, za.z, za.w);
+    } else {
+      x = a[i]; y = b[i]; z = c[i];
+    }
+    s += (x.x + y.y) * z.z + (x.w - y.x) * z.w + x.y * y.z + z.x;
+  }
+  if (s == 123.456f) out[0] = s;
+}
+
+template <bool NT>
+__global__ void k_copy2(int64_t n4, const float4* __restrict__ a, float4* __restrict__ b) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4; i += (int64_t)gridDim.x * 256) {
+    typedef float v4 __attribute__((ext_vector_type(4)));
+    if (NT) __builtin_nontemporal_store(__builtin_nontemporal_load(reinterpret_cast<const v4*>(a) + i), reinterpret_cast<v4*>(b) + i);
+    else b[i] = a[i];
+  }
+}
+
 int main() {
   const int64_t BT = 8192 * 32;
   float *x, *W, *z, *z2;
@@ -71,6 +101,37 @@ int main() {
     printf("%-28s %8.3f ms  %7.0f GB/s\n", name, ms / R, bytes / (ms / R * 1e-3) / 1e9);
   };
   timeit([&] { k_copy<<<8192, 256>>>(4 * BT * H / 4, (const float4*)z, (float4*)z2); }, "copy (ref)");
+  {
+    const int64_t n4 = BT * H / 4;   // one plane = 268 MB; 3 planes read = 805 MB (bytes scaled below)
+    float* o; hipMalloc(&o, 16);
+    for (int grid : {1024, 2048, 4096, 8192, 16384}) {
+      char nm[64];
+      auto t3 = [&](bool nt) {
+        hipEventRecord(e0);
+        for (int i = 0; i < 10; ++i) {
+          if (nt) k_read3<true><<<grid, 256>>>(n4, (const float4*)z, (const float4*)(z + BT * H), (const float4*)(z + 2 * BT * H), o);
+          else k_read3<false><<<grid, 256>>>(n4, (const float4*)z, (const float4*)(z + BT * H), (const float4*)(z + 2 * BT * H), o);
+        }
+        hipEventRecord(e1); hipEventSynchronize(e1);
+        float ms; hipEventElapsedTime(&ms, e0, e1);
+        printf("read3 %s grid=%-6d %8.3f ms  %7.0f GB/s\n", nt ? "nt " : "   ", grid, ms / 10, 3.0 * n4 * 16 / (ms / 10 * 1e-3) / 1e9);
+      };
+      t3(false); t3(true);
+      (void)nm;
+    }
+    for (int grid : {2048, 8192, 32768}) {
+      for (int nt = 0; nt < 2; ++nt) {
+        hipEventRecord(e0);
+        for (int i = 0; i < 10; ++i) {
+          if (nt) k_copy2<true><<<grid, 256>>>(4 * BT * H / 4, (const float4*)z, (float4*)z2);
+          else k_copy2<false><<<grid, 256>>>(4 * BT * H / 4, (const float4*)z, (float4*)z2);
+        }
+        hipEventRecord(e1); hipEventSynchronize(e1);
+        float ms; hipEventElapsedTime(&ms, e0, e1);
+        printf("copy %s grid=%-6d %8.3f ms  %7.0f GB/s\n", nt ? "nt" : "  ", grid, ms / 10, bytes / (ms / 10 * 1e-3) / 1e9);
+      }
+    }
+  }
   for (int grid : {512, 1024, 2048, 4096}) {
     char nm[64];
     snprintf(nm, 64, "apply RPI=1 grid=%d", grid);

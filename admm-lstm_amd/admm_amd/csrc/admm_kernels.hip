@@ -177,10 +177,14 @@ __device__ __forceinline__ SweepRes sweep_point(const Hyper& hp, const SweepIn& 
   return o;
 }
 
+// c_t and h_t are read back at t+1 (c_{t-1} of the update, h_{t-1} of the next GEMM): cached
+// stores; everything else is streamed.
 __device__ __forceinline__ void sweep_store(const SweepT& a, const SweepRes& o, int64_t ot, bool last) {
-  a.S.p[0][ot] = o.i1; a.S.p[1][ot] = o.f1; a.S.p[2][ot] = o.g1; a.S.p[3][ot] = o.o1; a.S.p[4][ot] = o.c1;
+  st_nt(a.S.p[0] + ot, o.i1); st_nt(a.S.p[1] + ot, o.f1); st_nt(a.S.p[2] + ot, o.g1); st_nt(a.S.p[3] + ot, o.o1);
+  a.S.p[4][ot] = o.c1;
   if (!last) a.S.p[5][ot] = o.h1;
-  a.L.p[0][ot] = o.li; a.L.p[1][ot] = o.lf; a.L.p[2][ot] = o.lg; a.L.p[3][ot] = o.lo; a.L.p[4][ot] = o.lc;
+  st_nt(a.L.p[0] + ot, o.li); st_nt(a.L.p[1] + ot, o.lf); st_nt(a.L.p[2] + ot, o.lg); st_nt(a.L.p[3] + ot, o.lo);
+  st_nt(a.L.p[4] + ot, o.lc);
 }
 
 // One ADMM time step t (admm.py:72-76): i, f, g, o (admm.py:353-386), c (388-436),
@@ -210,14 +214,16 @@ __global__ __launch_bounds__(kThreads) void k_sweep_t(Geom g, int t, Weights w, 
     const int64_t op = ot - g.H;
     SweepIn v;
     v.zi = acc[0][0][r]; v.zf = acc[0][1][r]; v.zg = acc[0][2][r]; v.zo = acc[0][3][r];
-    v.f0 = a.S.p[1][ot]; v.g0 = a.S.p[2][ot]; v.c0 = a.S.p[4][ot]; v.h0 = a.S.p[5][ot];
-    v.cp = a.S.p[4][op];
-    v.li = a.L.p[0][ot]; v.lf = a.L.p[1][ot]; v.lg = a.L.p[2][ot]; v.lo = a.L.p[3][ot];
-    v.lc = a.L.p[4][ot]; v.lh = a.L.p[5][ot];
+    v.f0 = ld_nt(a.S.p[1] + ot, 0); v.g0 = ld_nt(a.S.p[2] + ot, 0); v.c0 = ld_nt(a.S.p[4] + ot, 0);
+    v.h0 = ld_nt(a.S.p[5] + ot, 0);
+    v.cp = a.S.p[4][op];   // written at t-1 by this sweep: keep it cacheable
+    v.li = ld_nt(a.L.p[0] + ot, 0); v.lf = ld_nt(a.L.p[1] + ot, 0); v.lg = ld_nt(a.L.p[2] + ot, 0);
+    v.lo = ld_nt(a.L.p[3] + ot, 0); v.lc = ld_nt(a.L.p[4] + ot, 0); v.lh = ld_nt(a.L.p[5] + ot, 0);
     const SweepRes o = sweep_point(hp, v, last);
     sweep_store(a, o, ot, last);
     const int64_t e = (b * g.T + (t - 1)) * g.H + j;
-    a.zc[e] = v.zi; a.zc[BT * g.H + e] = v.zf; a.zc[2 * BT * g.H + e] = v.zg; a.zc[3 * BT * g.H + e] = v.zo;
+    st_nt(a.zc + e, v.zi); st_nt(a.zc + BT * g.H + e, v.zf); st_nt(a.zc + 2 * BT * g.H + e, v.zg);
+    st_nt(a.zc + 3 * BT * g.H + e, v.zo);
   }
 }
 
@@ -443,7 +449,7 @@ struct AtRFusedSrc {
     const float t0 = TANH ? 0.f : 0.5f;
     if (row >= rend || j >= H) return BRaw{make_float4(0.f, 0.f, 0.f, 0.f), make_float4(t0, t0, t0, t0)};
     const int64_t e = row * H + j;
-    return BRaw{*reinterpret_cast<const float4*>(zq + e), *reinterpret_cast<const float4*>(tq + e)};
+    return BRaw{ld_nt(zq + e), ld_nt(tq + e)};
   }
   __device__ float4 bfin(const BRaw& v) const {
     const float zz[4] = {v.z.x, v.z.y, v.z.z, v.z.w}, tt[4] = {v.t.x, v.t.y, v.t.z, v.t.w};
@@ -572,7 +578,7 @@ __device__ __forceinline__ void qgemm_body(const Geom& g, const float* x, const 
     const int64_t row = m0 + wm0 + acc_row(r, lane);
     if (row >= BT) continue;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) Q[((int64_t)q * BT + row) * g.H + j] = acc[0][q][r];
+    for (int q = 0; q < 4; ++q) st_nt(Q + ((int64_t)q * BT + row) * g.H + j, acc[0][q][r]);
   }
 }
 

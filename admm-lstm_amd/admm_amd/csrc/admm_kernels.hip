@@ -190,6 +190,9 @@ __device__ __forceinline__ void sweep_store(const SweepT& a, const SweepRes& o, 
 // One ADMM time step t (admm.py:72-76): i, f, g, o (admm.py:353-386), c (388-436),
 // h for t < T (455-457), dual ascent for i, f, g, o, c (504-530).  h_T, a and the
 // duals of h at T are finished by the h_T kernels below.
+#ifndef SWEEP_AHEAD
+#define SWEEP_AHEAD 1   // points whose operands are in flight while one is computed
+#endif
 template <bool VEC>
 __global__ __launch_bounds__(kThreads) void k_sweep_t(Geom g, int t, Weights w, Hyper hp, SweepT a) {
   __shared__ float smem[TSTile::LDS_FLOATS];
@@ -206,20 +209,32 @@ __global__ __launch_bounds__(kThreads) void k_sweep_t(Geom g, int t, Weights w, 
   if (j >= g.H) return;
   const int64_t BT = g.BT();
   const bool last = (t == g.T);
-#pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    const int64_t b = m0 + wm0 + acc_row(r, lane);
-    if (b >= a.r1) continue;
+  // The operands of point r+1 are loaded before point r's results are stored: vmcnt counts
+  // loads and stores in order, so a load issued after the stores would wait for them too
+  // (one full memory round trip per point).
+  // Rows past r1 load row r1-1 (branch-free, so the prefetched registers need no phi copies).
+  auto load_pt = [&](int r, SweepIn& v) {
+    const int64_t b = min(m0 + wm0 + acc_row(r, lane), a.r1 - 1);
     const int64_t ot = b * rs + (int64_t)t * g.H + j;
-    const int64_t op = ot - g.H;
-    SweepIn v;
-    v.zi = acc[0][0][r]; v.zf = acc[0][1][r]; v.zg = acc[0][2][r]; v.zo = acc[0][3][r];
     v.f0 = ld_nt(a.S.p[1] + ot, 0); v.g0 = ld_nt(a.S.p[2] + ot, 0); v.c0 = ld_nt(a.S.p[4] + ot, 0);
     v.h0 = ld_nt(a.S.p[5] + ot, 0);
-    v.cp = a.S.p[4][op];   // written at t-1 by this sweep: keep it cacheable
+    v.cp = a.S.p[4][ot - g.H];   // written at t-1 by this sweep: keep it cacheable
     v.li = ld_nt(a.L.p[0] + ot, 0); v.lf = ld_nt(a.L.p[1] + ot, 0); v.lg = ld_nt(a.L.p[2] + ot, 0);
     v.lo = ld_nt(a.L.p[3] + ot, 0); v.lc = ld_nt(a.L.p[4] + ot, 0); v.lh = ld_nt(a.L.p[5] + ot, 0);
+  };
+  constexpr int kAhead = SWEEP_AHEAD;
+  SweepIn ring[kAhead + 1];
+#pragma unroll
+  for (int r = 0; r < kAhead; ++r) load_pt(r, ring[r]);
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    if (r + kAhead < 16) load_pt(r + kAhead, ring[(r + kAhead) % (kAhead + 1)]);
+    SweepIn v = ring[r % (kAhead + 1)];
+    const int64_t b = m0 + wm0 + acc_row(r, lane);
+    const int64_t ot = b * rs + (int64_t)t * g.H + j;
+    v.zi = acc[0][0][r]; v.zf = acc[0][1][r]; v.zg = acc[0][2][r]; v.zo = acc[0][3][r];
     const SweepRes o = sweep_point(hp, v, last);
+    if (b >= a.r1) continue;
     sweep_store(a, o, ot, last);
     const int64_t e = (b * g.T + (t - 1)) * g.H + j;
     st_nt(a.zc + e, v.zi); st_nt(a.zc + BT * g.H + e, v.zf); st_nt(a.zc + 2 * BT * g.H + e, v.zg);

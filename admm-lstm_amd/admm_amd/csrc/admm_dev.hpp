@@ -67,6 +67,14 @@ __device__ __forceinline__ float expm1_acc(float x) {
   return __expf(x) - 1.f;
 }
 
+// a / b: v_rcp and one Newton step on the quotient (about 1 ulp; IEEE division costs 3x the
+// VALU issue, which the sweep's consumer waves share with the MFMA waves of their SIMD)
+__device__ __forceinline__ float div_fast(float a, float b) {
+  const float r = __builtin_amdgcn_rcpf(b);
+  const float q = a * r;
+  return fmaf(fmaf(-b, q, a), r, q);
+}
+
 // phi(z) and phi'(z) for the gradient / residual / line-search paths, from one v_exp and one
 // v_rcp (a few ulp; these feed sums, not the stored state).  With w = |z| (sigmoid) or 2|z|
 // (tanh), E = exp(-w), r = 1/(1+E):  sigma: phi = r or E r, phi' = E r^2;  tanh: |phi| =
@@ -155,6 +163,18 @@ __device__ __forceinline__ int xcd_swizzle(int bid, int nb) {
   const int x = bid % NX, i = bid / NX;
   // XCD x owns q (+1 if x < r) consecutive logical ids
   return x * q + (x < r ? x : r) + i;
+}
+
+// Raw buffer access (gfx9 descriptor word 3; aux 2 = nt).  Out-of-range offsets (>= the
+// descriptor's byte count) load 0 and drop stores.
+constexpr int kBufWord3 = 0x00020000;
+template <int AUX = 2>
+__device__ __forceinline__ float buf_ld(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, (int)off, 0, AUX));
+}
+template <int AUX = 2>
+__device__ __forceinline__ void buf_st(__amdgpu_buffer_rsrc_t r, uint32_t off, float v) {
+  __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, v), r, (int)off, 0, AUX);
 }
 
 __device__ __forceinline__ int acc_row(int r, int lane) { return (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5); }

@@ -75,6 +75,8 @@ struct AdmmCtx {
   int* found = nullptr;
   int* pick = nullptr;
   int sweep_split = 2;     // sample parts of the sweep, one stream each (ADMM_SWEEP_SPLIT)
+  bool sweep_rows = false; // whole sweep as one persistent launch (k_sweep_rows; ADMM_SWEEP_ROWS=0 disables)
+  float* swt = nullptr;    // its B-operand image of the weights
   hipStream_t sx[kMaxSweepStreams - 1] = {};
   hipEvent_t ev_fork = nullptr, ev_join[kMaxSweepStreams - 1] = {};
   float *U = nullptr, *wy_slab = nullptr, *Gy = nullptr;
@@ -257,7 +259,13 @@ int stage_sweep(AdmmCtx* c, hipStream_t s) {
   sa.S = planes(c->buf.gates);
   sa.L = planes(c->buf.duals);
   sa.zc = c->zc;
-  {
+  if (c->sweep_rows) {
+    ProfScope ps(c, ADMM_PROF_SWEEP, s);
+    sa.r0 = 0;
+    sa.r1 = g.B;
+    launch_sweep_wt(g, w, c->swt, s);
+    launch_sweep_rows(g, c->swt, c->hp, sa, s);
+  } else {
     // Samples are independent across the sweep: two halves on two streams run their
     // per-t kernels concurrently, so one half's HBM-bound epilogue overlaps the other's
     // MFMA-bound GEMM on the same CUs (one kernel per t alone runs them back to back).
@@ -340,6 +348,8 @@ int admm_create(const AdmmDims* dims, const AdmmParams* params, int device, Admm
   g.set_T();
   if (const char* e = std::getenv("ADMM_SWEEP_SPLIT"))
     c->sweep_split = std::max(1, std::min(kMaxSweepStreams, std::atoi(e)));
+  c->sweep_rows = sweep_rows_ok(g);
+  if (const char* e = std::getenv("ADMM_SWEEP_ROWS")) c->sweep_rows = c->sweep_rows && std::atoi(e) != 0;
   Hyper& h = c->hp;
   for (int i = 0; i < 7; ++i) h.rho[i] = params->rho[i];
   for (int q = 0; q < 4; ++q) {
@@ -369,7 +379,8 @@ int admm_create(const AdmmDims* dims, const AdmmParams* params, int device, Admm
       (rc = dalloc(&c->found, 4)) || (rc = dalloc(&c->pick, 4)) ||
       (rc = dalloc(&c->U, (size_t)g.B * g.O)) || (rc = dalloc(&c->wy_slab, (size_t)c->wy_nsplit * g.H * g.O)) ||
       (rc = dalloc(&c->Gy, (size_t)g.H * g.O)) || (rc = dalloc(&c->ht_part, (size_t)c->ht_nblk * kHTSums)) ||
-      (rc = dalloc(&c->ht_sums, kHTSums)) || (rc = dalloc(&c->stats, 1))) {
+      (rc = dalloc(&c->ht_sums, kHTSums)) || (rc = dalloc(&c->stats, 1)) ||
+      (c->sweep_rows && (rc = dalloc(&c->swt, sweep_wt_floats(g))))) {
     std::string msg = g_last_error;
     admm_destroy(c);
     return fail(rc, "%s", msg.c_str());
@@ -394,7 +405,7 @@ int admm_destroy(AdmmCtx* c) {
   if (!c) return ADMM_OK;
   (void)hipSetDevice(c->device);
   void* ptrs[] = {c->zc, c->tgt, c->R, c->Q, c->G, c->dW, c->gslab, c->tr_part, c->tr_sums, c->tr_poly, c->found, c->pick,
-                  c->U, c->wy_slab, c->Gy, c->ht_part, c->ht_sums, c->stats};
+                  c->U, c->wy_slab, c->Gy, c->ht_part, c->ht_sums, c->stats, c->swt};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   if (c->comm) ncclCommDestroy(c->comm);

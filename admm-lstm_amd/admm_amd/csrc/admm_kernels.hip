@@ -144,6 +144,12 @@ struct SweepIn {
   float f0, g0, c0, h0, cp;   // old f, g, c, h at t; new c at t-1
   float li, lf, lg, lo, lc, lh;
 };
+// sigma(z) for the sweep: accurate expf, 1/(1+e) by v_rcp and one Newton step (div_fast)
+__device__ __forceinline__ float sig_sweep(float z) {
+  const float e = expf(-fabsf(z));
+  const float r = div_fast(1.f, 1.f + e);
+  return z >= 0.f ? r : e * r;
+}
 struct SweepRes {
   float i1, f1, g1, o1, c1, h1;
   float li, lf, lg, lo, lc;
@@ -151,23 +157,23 @@ struct SweepRes {
 
 __device__ __forceinline__ SweepRes sweep_point(const Hyper& hp, const SweepIn& v, bool last) {
   const float ri = hp.rho[0], rf = hp.rho[1], rg = hp.rho[2], ro = hp.rho[3], rc = hp.rho[4], rh = hp.rho[5];
-  const float ai = sigm(v.zi), af = sigm(v.zf), ag = tanhf(v.zg), ao = sigm(v.zo);
+  const float ai = sig_sweep(v.zi), af = sig_sweep(v.zf), ag = tanhf(v.zg), ao = sig_sweep(v.zo);
   const float f0 = v.f0, g0 = v.g0, c0 = v.c0, h0 = v.h0, cp = v.cp;
   const float li = v.li, lf = v.lf, lg = v.lg, lo = v.lo, lc = v.lc, lh = v.lh;
   SweepRes o;
   // admm.py:384-386 with (p1,p2,p3) of :360-375 and (var2, rho2, lam2) of :376-383
-  o.i1 = -((li - ri * ai) + (rc * (f0 * cp - c0) - lc) * g0) / (ri + rc * g0 * g0);
-  o.f1 = -((lf - rf * af) + (rc * (g0 * o.i1 - c0) - lc) * cp) / (rf + rc * cp * cp);
-  o.g1 = -((lg - rg * ag) + (rc * (o.f1 * cp - c0) - lc) * o.i1) / (rg + rc * o.i1 * o.i1);
+  o.i1 = div_fast(-((li - ri * ai) + (rc * (f0 * cp - c0) - lc) * g0), ri + rc * g0 * g0);
+  o.f1 = div_fast(-((lf - rf * af) + (rc * (g0 * o.i1 - c0) - lc) * cp), rf + rc * cp * cp);
+  o.g1 = div_fast(-((lg - rg * ag) + (rc * (o.f1 * cp - c0) - lc) * o.i1), rg + rc * o.i1 * o.i1);
   const float tc0 = tanhf(c0);
-  o.o1 = -((lo - ro * ao) + (rh * (0.f - h0) - lh) * tc0) / (ro + rh * tc0 * tc0);
+  o.o1 = div_fast(-((lo - ro * ao) + (rh * (0.f - h0) - lh) * tc0), ro + rh * tc0 * tc0);
   // admm.py:388-436: autograd gradient of .5||tanh(c) o - (h + lam_h/rho_h)||^2, theta* = 0.5
-  const float div_h = lh / rh, div_c = lc / rc;
+  const float div_h = div_fast(lh, rh), div_c = div_fast(lc, rc);
   const float vv = tc0 * o.o1 - (h0 + div_h);
   const float gc = (vv * o.o1) * (1.f - tc0 * tc0);
   const float A = (div_c - o.f1 * cp) - o.i1 * o.g1;
-  o.c1 = (0.5f * c0 - gc - rc * A) / (rc + 0.5f);
-  o.h1 = last ? h0 : (rh * o.o1 * tanhf(o.c1) - lh) / rh;  // admm.py:455-457
+  o.c1 = div_fast(0.5f * c0 - gc - rc * A, rc + 0.5f);
+  o.h1 = last ? h0 : div_fast(rh * o.o1 * tanhf(o.c1) - lh, rh);  // admm.py:455-457
   // admm.py:512-530
   o.li = li + ri * (o.i1 - ai);
   o.lf = lf + rf * (o.f1 - af);
@@ -239,6 +245,208 @@ __global__ __launch_bounds__(kThreads) void k_sweep_t(Geom g, int t, Weights w, 
     const int64_t e = (b * g.T + (t - 1)) * g.H + j;
     st_nt(a.zc + e, v.zi); st_nt(a.zc + BT * g.H + e, v.zf); st_nt(a.zc + 2 * BT * g.H + e, v.zg);
     st_nt(a.zc + 3 * BT * g.H + e, v.zo);
+  }
+}
+
+// ---- the whole sweep in one persistent launch (H % 32 == 0, H <= 256, D <= 32) ----
+// Samples are independent across t, so a workgroup owns 32 rows for all of t = 1..T and no
+// grid-wide step is needed.  [x_t | h_{t-1}] of its rows lives in LDS (two buffers by t
+// parity): h never makes an HBM round trip inside the sweep, and c_{t-1} stays in the
+// consumer's registers.  Eight waves, two roles, one tile (4 gates x 32 hidden units) per step:
+//   waves 0-3 (producer, wave q = gate q): z tile of step s, MFMA 32x32x2 over K = 32 + H in
+//              32-deep groups (x zero-padded to one group), written to the LDS tile buffer s&1;
+//   waves 4-7 (consumer): the element-wise ADMM update of tile s-1 (sweep_point), its HBM
+//              loads issued one tile ahead, h_t written into the other LDS A-buffer.
+// The producer's matrix pipe and the consumer's memory stream overlap on every SIMD.  At a
+// t boundary the producer's tile (t+1, 0) needs h_t of the tile the consumer is finishing:
+// it runs K up to that tile's 32 columns, meets the consumer at a mid-step barrier, then
+// finishes the last group.
+constexpr int SR_ROWS = 32, SR_THREADS = 512, SR_DP = 32;
+#ifndef SR_PF
+#define SR_PF 3   // B groups in flight per producer wave
+#endif
+
+// B operand image for k_sweep_rows, one 1 KB wave-load per (gate q, tile n, 8-k block kb):
+// lane (kh, c) holds {W[8kb + 4kh + u][32n + c]}_u, W = [Wx_q zero-padded to 32 rows; Wh_q].
+__global__ __launch_bounds__(kThreads) void k_sweep_wt(int D, int H, Weights w, float* __restrict__ wt) {
+  const int NT = H / 32, KB = (SR_DP + H) / 8;
+  const int total = 4 * NT * KB * 64;
+  for (int i = blockIdx.x * kThreads + threadIdx.x; i < total; i += gridDim.x * kThreads) {
+    const int lane = i & 63, kb = (i >> 6) % KB, n = (i / (64 * KB)) % NT, q = i / (64 * KB * NT);
+    const int c = lane & 31, kh = lane >> 5, jj = 32 * n + c;
+    float v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int k = 8 * kb + 4 * kh + u;
+      v[u] = k < SR_DP ? (k < D ? w.wx[q][(int64_t)k * H + jj] : 0.f) : w.wh[q][(int64_t)(k - SR_DP) * H + jj];
+    }
+    reinterpret_cast<float4*>(wt)[i] = make_float4(v[0], v[1], v[2], v[3]);
+  }
+}
+
+struct SrState { float f0, g0, c0, h0, li, lf, lg, lo, lc, lh; };
+
+template <int NT>
+__global__ __launch_bounds__(SR_THREADS) void k_sweep_rows(Geom g, const float* __restrict__ wt, Hyper hp,
+                                                            SweepT a) {
+  // AS % 64 in {4, 36}: the 16 lanes of a ds_read_b128 phase hit distinct bank quads
+  constexpr int H = 32 * NT, KP = SR_DP + H, KG = KP / 32, AS = KP + 4;
+  __shared__ float Ab[2][SR_ROWS * AS];
+  __shared__ float Zb[2][4 * SR_ROWS * 32];
+  __shared__ float Cs[NT * 4][256];          // consumer-private c_{t-1}
+  const int T = g.T, D = g.D;
+  const int64_t m0 = a.r0 + (int64_t)blockIdx.x * SR_ROWS;
+  const int64_t rs = (int64_t)(T + 1) * H;
+  const int64_t BTH = g.BT() * H;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+
+  // A image for t = 1: [x_1 | h_0]
+  for (int i = threadIdx.x; i < SR_ROWS * KP; i += SR_THREADS) {
+    const int row = i / KP, k = i % KP;
+    const int64_t b = min(m0 + row, a.r1 - 1);
+    Ab[1][row * AS + k] = k < SR_DP ? (k < D ? a.x[b * T * D + k] : 0.f) : a.S.p[5][b * rs + (k - SR_DP)];
+  }
+  __syncthreads();
+
+  if (wave < 4) {
+    // ------------------------------------------------------------------ producer (gate q)
+    // The B stream of a wave is the cyclic sequence of its GT = NT*KG groups per t (4 float4
+    // per lane each).  The loop walks it U groups at a time with a U-deep register ring:
+    // slot u holds group G+u and is refilled with group G+u+U right after its 16 MFMAs.
+    const int q = wave, c = lane & 31, kh = lane >> 5;
+    const float4* wq = reinterpret_cast<const float4*>(wt) + (size_t)q * NT * KG * 4 * 64 + lane;
+    constexpr int GT = NT * KG;
+    constexpr int U = (GT % SR_PF == 0) ? SR_PF : ((GT % 3 == 0) ? 3 : 2);
+    static_assert(GT % U == 0, "group ring must divide the groups of a t");
+    float4 bq[U][4];
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) bq[u][i] = wq[(u * 4 + i) * 64];
+    f32x16 acc = {};
+    for (int t = 1; t <= T; ++t) {
+      const float* A = &Ab[t & 1][c * AS + 4 * kh];
+#pragma unroll 1
+      for (int G0 = 0; G0 < GT; G0 += U) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const int G = G0 + u, n = G / KG, gg = G - n * KG;
+          if (n == 0 && gg == KG - 1) __syncthreads();   // mid-step: h_{t-1} of tile NT-1 is in
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const float4 a4 = *reinterpret_cast<const float4*>(A + 32 * gg + 8 * i);
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a4.x, bq[u][i].x, acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a4.y, bq[u][i].y, acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a4.z, bq[u][i].z, acc, 0, 0, 0);
+            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a4.w, bq[u][i].w, acc, 0, 0, 0);
+          }
+          const int Gn = G + U < GT ? G + U : G + U - GT;
+#pragma unroll
+          for (int i = 0; i < 4; ++i) bq[u][i] = wq[(Gn * 4 + i) * 64];
+          if (gg == KG - 1) {
+            float* Z = &Zb[((t - 1) * NT + n) & 1][q * SR_ROWS * 32 + c];
+#pragma unroll
+            for (int r = 0; r < 16; ++r) Z[acc_row(r, lane) * 32] = acc[r];
+            acc = f32x16{};
+            __syncthreads();   // end of step
+          }
+        }
+      }
+    }
+    __syncthreads();         // final step: the consumer drains the last tile
+    return;
+  }
+
+  // -------------------------------------------------------------------- consumer
+  // Plane accesses go through buffer descriptors: one 32-bit byte offset per point serves
+  // every plane (no 64-bit address per plane and point), and the descriptor's record count
+  // (rows < r1) turns loads past the last row into zeros and drops their stores.
+  const int ct = threadIdx.x - 4 * 64;      // 0..255
+  const int jl = ct & 31, rb = ct >> 5;      // rows rb + 8r, r = 0..3
+  const uint32_t pbytes = (uint32_t)(a.r1 * rs * 4), zbytes = (uint32_t)(a.r1 * T * H * 4);
+  __amdgpu_buffer_rsrc_t rS[6], rL[6], rZ[4];
+#pragma unroll
+  for (int p = 0; p < 6; ++p) {
+    rS[p] = __builtin_amdgcn_make_buffer_rsrc(a.S.p[p], 0, pbytes, kBufWord3);
+    rL[p] = __builtin_amdgcn_make_buffer_rsrc(a.L.p[p], 0, pbytes, kBufWord3);
+  }
+#pragma unroll
+  for (int q = 0; q < 4; ++q) rZ[q] = __builtin_amdgcn_make_buffer_rsrc(a.zc + q * BTH, 0, zbytes, kBufWord3);
+  uint32_t pofs[4], zofs[4];                 // byte offsets of the points at t = 0 / t = 1, tile 0
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int64_t b = m0 + rb + 8 * r;
+    pofs[r] = (uint32_t)((b * rs + jl) * 4);
+    zofs[r] = (uint32_t)((b * T * H + jl) * 4);
+  }
+  // c_{t-1} of the consumer's points, by tile: Cs[n*4 + r][ct]
+  for (int n = 0; n < NT; ++n)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) Cs[n * 4 + r][ct] = buf_ld<0>(rS[4], pofs[r] + 128 * n);   // c_0
+
+  auto load_tile = [&](int t, int n, SrState (&v)[4]) {
+    const uint32_t d = (uint32_t)(t * H + 32 * n) * 4;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const uint32_t o = pofs[r] + d;
+      v[r].f0 = buf_ld(rS[1], o); v[r].g0 = buf_ld(rS[2], o); v[r].c0 = buf_ld(rS[4], o); v[r].h0 = buf_ld(rS[5], o);
+      v[r].li = buf_ld(rL[0], o); v[r].lf = buf_ld(rL[1], o); v[r].lg = buf_ld(rL[2], o);
+      v[r].lo = buf_ld(rL[3], o); v[r].lc = buf_ld(rL[4], o); v[r].lh = buf_ld(rL[5], o);
+    }
+  };
+  // x_{tn} into A-buffer tn&1 (32 rows x 32, four values per consumer thread)
+  auto load_x = [&](int tn) {
+    if (tn > T) return;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int i = ct + 256 * u, row = i >> 5, k = i & 31;
+      const int64_t b = min(m0 + row, a.r1 - 1);
+      Ab[tn & 1][row * AS + k] = k < D ? a.x[(b * T + (tn - 1)) * D + k] : 0.f;
+    }
+  };
+
+  SrState nxt[4];
+  load_tile(1, 0, nxt);
+  load_x(2);                 // step 0: the producer computes tile (1, 0)
+  __syncthreads();           // its mid-step barrier
+  __syncthreads();           // end of step 0
+  for (int t = 1; t <= T; ++t) {
+    const bool last = (t == T);
+    float* An = &Ab[(t + 1) & 1][SR_DP + jl];
+#pragma unroll 1
+    for (int n = 0; n < NT; ++n) {
+      SrState cur[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) cur[r] = nxt[r];
+      if (n + 1 < NT) load_tile(t, n + 1, nxt);
+      else if (!last) load_tile(t + 1, 0, nxt);
+      const float* Z = &Zb[((t - 1) * NT + n) & 1][(rb * 32) + jl];
+      const uint32_t d = (uint32_t)(t * H + 32 * n) * 4, dz = (uint32_t)((t - 1) * H + 32 * n) * 4;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        SweepIn v;
+        v.zi = Z[(8 * r) * 32]; v.zf = Z[SR_ROWS * 32 + (8 * r) * 32];
+        v.zg = Z[2 * SR_ROWS * 32 + (8 * r) * 32]; v.zo = Z[3 * SR_ROWS * 32 + (8 * r) * 32];
+        float* cp = &Cs[n * 4 + r][ct];
+        v.f0 = cur[r].f0; v.g0 = cur[r].g0; v.c0 = cur[r].c0; v.h0 = cur[r].h0; v.cp = *cp;
+        v.li = cur[r].li; v.lf = cur[r].lf; v.lg = cur[r].lg; v.lo = cur[r].lo; v.lc = cur[r].lc; v.lh = cur[r].lh;
+        const SweepRes o = sweep_point(hp, v, last);
+        *cp = o.c1;
+        if (!last) An[(rb + 8 * r) * AS + 32 * n] = o.h1;
+        const uint32_t po = pofs[r] + d, zo = zofs[r] + dz;
+        buf_st(rS[0], po, o.i1); buf_st(rS[1], po, o.f1); buf_st(rS[2], po, o.g1); buf_st(rS[3], po, o.o1);
+        buf_st<0>(rS[4], po, o.c1);          // c_t and h_t are read back by the next step's kernels
+        if (!last) buf_st<0>(rS[5], po, o.h1);
+        buf_st(rL[0], po, o.li); buf_st(rL[1], po, o.lf); buf_st(rL[2], po, o.lg); buf_st(rL[3], po, o.lo);
+        buf_st(rL[4], po, o.lc);
+        buf_st(rZ[0], zo, v.zi); buf_st(rZ[1], zo, v.zf); buf_st(rZ[2], zo, v.zg); buf_st(rZ[3], zo, v.zo);
+      }
+      if (n == NT - 1 && !last) {
+        load_x(t + 2);       // the producer's next tile is (t+1, 0)
+        __syncthreads();     // its mid-step barrier: h_t is complete
+      }
+      __syncthreads();       // end of step
+    }
   }
 }
 
@@ -1453,6 +1661,28 @@ void launch_sweep_t(const Geom& g, int t, const Weights& w, const Hyper& hp, con
   dim3 grid(cdiv64(a.r1 - a.r0, TS_BM) * cdiv64(g.H, 32));
   if (vec_ok(g)) k_sweep_t<true><<<grid, kThreads, 0, s>>>(g, t, w, hp, a);
   else k_sweep_t<false><<<grid, kThreads, 0, s>>>(g, t, w, hp, a);
+}
+
+bool sweep_rows_ok(const Geom& g) {
+  // 32-bit buffer offsets: a [B][T+1][H] plane and a [B*T][H] z-cache plane in bytes
+  return g.H % 32 == 0 && g.H <= 256 && g.D <= SR_DP && g.B * (int64_t)g.TP() * g.H * 4 < (int64_t)UINT32_MAX;
+}
+
+size_t sweep_wt_floats(const Geom& g) { return (size_t)4 * (g.H / 32) * ((SR_DP + g.H) / 8) * 256; }
+
+void launch_sweep_wt(const Geom& g, const Weights& w, float* wt, hipStream_t s) {
+  const int total = 4 * (g.H / 32) * ((SR_DP + g.H) / 8) * 64;
+  k_sweep_wt<<<cdiv64(total, kThreads), kThreads, 0, s>>>(g.D, g.H, w, wt);
+}
+
+void launch_sweep_rows(const Geom& g, const float* wt, const Hyper& hp, const SweepT& a, hipStream_t s) {
+  dim3 grid(cdiv64(a.r1 - a.r0, SR_ROWS));
+  switch (g.H / 32) {
+#define SR_CASE(N) case N: k_sweep_rows<N><<<grid, SR_THREADS, 0, s>>>(g, wt, hp, a); break;
+    SR_CASE(1) SR_CASE(2) SR_CASE(3) SR_CASE(4) SR_CASE(5) SR_CASE(6) SR_CASE(7) SR_CASE(8)
+#undef SR_CASE
+    default: break;
+  }
 }
 
 void launch_rowdot(int64_t B, int H, int O, const float* h, int64_t hs, const float* wy, float* out, hipStream_t s) {

@@ -277,9 +277,11 @@ def test_forward_matches_oracle(dev):
         assert float((m(x.to(dev)).cpu() - ref['a']).abs().max()) <= 1e-5
 
 
-@pytest.mark.parametrize('shape', [(200, 5, 3, 40, 2), (33, 1, 2, 7, 1), (129, 4, 5, 33, 3)])
+@pytest.mark.parametrize('shape', [(200, 5, 3, 40, 2), (33, 1, 2, 7, 1), (129, 4, 5, 33, 3),
+                                   (100, 3, 5, 64, 1), (40, 1, 16, 32, 1)])
 def test_edge_shapes_vs_oracle(shape, mods, dev):
-    """Ragged tiles (B, H not multiples of 128/32), T = 1, multi-output O."""
+    """Ragged tiles (B, H not multiples of 128/32), T = 1, multi-output O.  H % 32 == 0 runs the
+    persistent sweep (k_sweep_rows) with a ragged last row block; the others the per-t sweep."""
     from blocks.lstm import LSTM
     from parameters import example_parameter_dictionary
     admm, _ = mods
@@ -374,3 +376,30 @@ def test_full_size_c3_properties(mods, dev):
     assert torch.equal(h1, h2)
     assert all(math.isfinite(v) for v in l1)
     assert l1[3] < l1[0]
+
+
+def test_persistent_sweep_matches_per_t_sweep(mods, dev, monkeypatch):
+    """The two sweep implementations (one persistent launch vs one launch per t, chosen at
+    create time by ADMM_SWEEP_ROWS) agree on a C3-shaped step (H = 256, D = 16)."""
+    from blocks.lstm import LSTM
+    from parameters import example_parameter_dictionary
+    admm, _ = mods
+    admm.with_dual_y = False
+    B, T, D, H = 300, 4, 16, 256
+    g = torch.Generator().manual_seed(11)
+    x = torch.rand(B, T, D, generator=g).to(dev)
+    y = torch.rand(B, 1, generator=g).to(dev)
+    pd = example_parameter_dictionary['GoogleStock']
+    out = {}
+    for flag in ('1', '0'):
+        monkeypatch.setenv('ADMM_SWEEP_ROWS', flag)
+        torch.manual_seed(0)
+        m = LSTM(D, H, 1).to(dev)
+        opt = admm.ADMMBasedOptimizer(m, (x, y), pd, verbose=False)
+        for _ in range(2):
+            opt.step()
+        out[flag] = ({q: opt.gates[q].clone() for q in GATES6}, {q: opt.duals[q].clone() for q in GATES6})
+    for k in (0, 1):
+        for q in GATES6:
+            d = float((out['1'][k][q] - out['0'][k][q]).abs().max())
+            assert d <= 1e-5, (k, q, d)

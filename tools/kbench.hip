@@ -96,6 +96,11 @@ int main(int argc, char** argv) {
     timeit("sweep T steps, 1 stream", sb, sf, [&] {
       for (int t = 1; t <= g.T; ++t) launch_sweep_t(g, t, w, hp, sw, s);
     });
+    if (sweep_rows_ok(g)) {
+      float* wt; (void)hipMalloc(&wt, sweep_wt_floats(g) * 4);
+      timeit("sweep_wt", 0, 0, [&] { launch_sweep_wt(g, w, wt, s); });
+      timeit("sweep rows (1 launch)", sb, sf, [&] { launch_sweep_rows(g, wt, hp, sw, s); });
+    }
     timeit("sweep T steps, 2 streams", sb, sf, [&] {
       const int64_t mid = (g.B / 2 + 127) / 128 * 128;
       (void)hipEventRecord(ef, s);

@@ -16,6 +16,8 @@ namespace admm {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 
 // Streaming (non-temporal) accesses for data touched once per pass: the ADMM state planes,
 // the z cache and the line-search targets.  Calibrated on the box (tools/streambench.hip):
@@ -65,6 +67,26 @@ __device__ __forceinline__ float expm1_acc(float x) {
     return p * x;
   }
   return __expf(x) - 1.f;
+}
+
+// Three-way bf16 split of f32 values: a = p0 + p1 + p2 to ~2^-27 relative (each remainder is
+// exact in f32).  Products of two split operands summed over the six terms with i + j <= 2
+// (p_i q_j exact in the MFMA's f32 accumulation) reproduce an f32 product to ~2^-26 relative,
+// at the bf16 matrix rate: 6 x v_mfma_f32_32x32x16_bf16 (192 cycles) per 16-deep step against
+// 8 x v_mfma_f32_32x32x2_f32 (512 cycles, and those hold the SIMD's VALU issue).
+template <class V, class B>
+__device__ __forceinline__ void split3(V a, B& p0, B& p1, B& p2) {
+  p0 = __builtin_convertvector(a, B);
+  const V r1 = a - __builtin_convertvector(p0, V);
+  p1 = __builtin_convertvector(r1, B);
+  const V r2 = r1 - __builtin_convertvector(p1, V);
+  p2 = __builtin_convertvector(r2, B);
+}
+__device__ __forceinline__ void split3(float a, __bf16& p0, __bf16& p1, __bf16& p2) {
+  p0 = (__bf16)a;
+  const float r1 = a - (float)p0;
+  p1 = (__bf16)r1;
+  p2 = (__bf16)(r1 - (float)p1);
 }
 
 // a / b: v_rcp and one Newton step on the quotient (about 1 ulp; IEEE division costs 3x the
@@ -171,6 +193,15 @@ constexpr int kBufWord3 = 0x00020000;
 template <int AUX = 2>
 __device__ __forceinline__ float buf_ld(__amdgpu_buffer_rsrc_t r, uint32_t off) {
   return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, (int)off, 0, AUX));
+}
+template <int AUX = 2>
+__device__ __forceinline__ f32x4 buf_ld4(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+  return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, AUX));
+}
+template <int AUX = 2>
+__device__ __forceinline__ void buf_st4(__amdgpu_buffer_rsrc_t r, uint32_t off, f32x4 v) {
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned int, v), r,
+                                         (int)off, 0, AUX);
 }
 template <int AUX = 2>
 __device__ __forceinline__ void buf_st(__amdgpu_buffer_rsrc_t r, uint32_t off, float v) {

@@ -251,118 +251,149 @@ __global__ __launch_bounds__(kThreads) void k_sweep_t(Geom g, int t, Weights w, 
 // ---- the whole sweep in one persistent launch (H % 32 == 0, H <= 256, D <= 32) ----
 // Samples are independent across t, so a workgroup owns 32 rows for all of t = 1..T and no
 // grid-wide step is needed.  [x_t | h_{t-1}] of its rows lives in LDS (two buffers by t
-// parity): h never makes an HBM round trip inside the sweep, and c_{t-1} stays in the
-// consumer's registers.  Eight waves, two roles, one tile (4 gates x 32 hidden units) per step:
-//   waves 0-3 (producer, wave q = gate q): z tile of step s, MFMA 32x32x2 over K = 32 + H in
-//              32-deep groups (x zero-padded to one group), written to the LDS tile buffer s&1;
+// parity, already split into three bf16 pieces): h never makes an HBM round trip inside the
+// sweep.  Eight waves, two roles, one tile (4 gates x 32 hidden units) per step:
+//   waves 0-3 (producer, wave q = gate q): z tile of step s over K = 16*XC + H in 16-deep
+//              chunks, each chunk 6 bf16 MFMAs of the split operands (split3: f32-accurate),
+//              written to the LDS tile buffer s&1;
 //   waves 4-7 (consumer): the element-wise ADMM update of tile s-1 (sweep_point), its HBM
-//              loads issued one tile ahead, h_t written into the other LDS A-buffer.
+//              loads issued one tile ahead, h_t split into the other LDS A-buffer.
 // The producer's matrix pipe and the consumer's memory stream overlap on every SIMD.  At a
 // t boundary the producer's tile (t+1, 0) needs h_t of the tile the consumer is finishing:
 // it runs K up to that tile's 32 columns, meets the consumer at a mid-step barrier, then
-// finishes the last group.
-constexpr int SR_ROWS = 32, SR_THREADS = 512, SR_DP = 32;
-#ifndef SR_PF
-#define SR_PF 3   // B groups in flight per producer wave
+// finishes the last two chunks.
+constexpr int SR_ROWS = 32, SR_THREADS = 512;
+#ifdef SR_TIMING
+__device__ unsigned long long g_sr_wait[2048][2];   // per workgroup: cycles the producer / consumer wave 0 waited at barriers
+#define SR_SYNC() do { const unsigned long long t0_ = clock64(); __syncthreads(); \
+    if ((threadIdx.x & 63) == 0) sr_wait += clock64() - t0_; } while (0)
+#else
+#define SR_SYNC() __syncthreads()
 #endif
 
-// B operand image for k_sweep_rows, one 1 KB wave-load per (gate q, tile n, 8-k block kb):
-// lane (kh, c) holds {W[8kb + 4kh + u][32n + c]}_u, W = [Wx_q zero-padded to 32 rows; Wh_q].
-__global__ __launch_bounds__(kThreads) void k_sweep_wt(int D, int H, Weights w, float* __restrict__ wt) {
-  const int NT = H / 32, KB = (SR_DP + H) / 8;
-  const int total = 4 * NT * KB * 64;
+template <int NT, int XC>
+struct SrGeom {
+  static constexpr int H = 32 * NT, XK = 16 * XC, K2 = XK + H;
+  static constexpr int KC2 = K2 / 16;          // 16-deep chunks per tile
+  static constexpr int AST = K2 + 8;           // A row stride (bf16): 16-B reads conflict-free over 16 rows
+  static constexpr int APIECE = SR_ROWS * AST; // one split piece of one A buffer
+  static constexpr int GT = NT * KC2;          // chunks per t
+  static constexpr int U = GT % 8 == 0 ? 8 : GT % 4 == 0 ? 4 : GT % 3 == 0 ? 3 : GT % 2 == 0 ? 2 : 1;
+};
+
+// B operand image: for gate q, tile n, chunk c, piece p and lane (h, c32) the 8 bf16
+// pieces of W[16c + 8h + j][32n + c32], j = 0..7, W = [Wx_q zero-padded to 16*XC rows; Wh_q].
+__global__ __launch_bounds__(kThreads) void k_sweep_wt(int D, int H, int XC, Weights w, bf16x8* __restrict__ wt) {
+  const int NT = H / 32, KC2 = XC + 2 * NT, XK = 16 * XC;
+  const int total = 4 * NT * KC2 * 64;
   for (int i = blockIdx.x * kThreads + threadIdx.x; i < total; i += gridDim.x * kThreads) {
-    const int lane = i & 63, kb = (i >> 6) % KB, n = (i / (64 * KB)) % NT, q = i / (64 * KB * NT);
-    const int c = lane & 31, kh = lane >> 5, jj = 32 * n + c;
-    float v[4];
+    const int lane = i & 63, c = (i >> 6) % KC2, n = (i / (64 * KC2)) % NT, q = i / (64 * KC2 * NT);
+    const int jj = 32 * n + (lane & 31), h = lane >> 5;
+    bf16x8 p0, p1, p2;
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int k = 8 * kb + 4 * kh + u;
-      v[u] = k < SR_DP ? (k < D ? w.wx[q][(int64_t)k * H + jj] : 0.f) : w.wh[q][(int64_t)(k - SR_DP) * H + jj];
+    for (int j = 0; j < 8; ++j) {
+      const int k = 16 * c + 8 * h + j;
+      const float v = k < XK ? (k < D ? w.wx[q][(int64_t)k * H + jj] : 0.f) : w.wh[q][(int64_t)(k - XK) * H + jj];
+      __bf16 a0, a1, a2;
+      split3(v, a0, a1, a2);
+      p0[j] = a0; p1[j] = a1; p2[j] = a2;
     }
-    reinterpret_cast<float4*>(wt)[i] = make_float4(v[0], v[1], v[2], v[3]);
+    const int base = (((q * NT + n) * KC2 + c) * 3) * 64 + lane;
+    wt[base] = p0; wt[base + 64] = p1; wt[base + 128] = p2;
   }
 }
 
-struct SrState { float f0, g0, c0, h0, li, lf, lg, lo, lc, lh; };
-
-template <int NT>
-__global__ __launch_bounds__(SR_THREADS) void k_sweep_rows(Geom g, const float* __restrict__ wt, Hyper hp,
+template <int NT, int XC>
+__global__ __launch_bounds__(SR_THREADS) void k_sweep_rows(Geom g, const bf16x8* __restrict__ wt, Hyper hp,
                                                             SweepT a) {
-  // AS % 64 in {4, 36}: the 16 lanes of a ds_read_b128 phase hit distinct bank quads
-  constexpr int H = 32 * NT, KP = SR_DP + H, KG = KP / 32, AS = KP + 4;
-  __shared__ float Ab[2][SR_ROWS * AS];
-  __shared__ float Zb[2][4 * SR_ROWS * 32];
-  __shared__ float Cs[NT * 4][256];          // consumer-private c_{t-1}
+  using SG = SrGeom<NT, XC>;
+  constexpr int H = SG::H, XK = SG::XK, K2 = SG::K2, KC2 = SG::KC2, AST = SG::AST, AP = SG::APIECE;
+  __shared__ __attribute__((aligned(16))) __bf16 Ab[2][3 * AP];
+  __shared__ __attribute__((aligned(16))) float Zb[2][4 * SR_ROWS * 32];
   const int T = g.T, D = g.D;
   const int64_t m0 = a.r0 + (int64_t)blockIdx.x * SR_ROWS;
   const int64_t rs = (int64_t)(T + 1) * H;
   const int64_t BTH = g.BT() * H;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+#ifdef SR_TIMING
+  unsigned long long sr_wait = 0, sr_t0 = clock64(), sr_comp = 0, sr_store = 0, sr_lw = 0;
+#endif
+  auto put_a = [&](int buf, int row, int k, float v) {
+    __bf16 p0, p1, p2;
+    split3(v, p0, p1, p2);
+    __bf16* d = &Ab[buf][row * AST + k];
+    d[0] = p0; d[AP] = p1; d[2 * AP] = p2;
+  };
 
   // A image for t = 1: [x_1 | h_0]
-  for (int i = threadIdx.x; i < SR_ROWS * KP; i += SR_THREADS) {
-    const int row = i / KP, k = i % KP;
+  for (int i = threadIdx.x; i < SR_ROWS * K2; i += SR_THREADS) {
+    const int row = i / K2, k = i % K2;
     const int64_t b = min(m0 + row, a.r1 - 1);
-    Ab[1][row * AS + k] = k < SR_DP ? (k < D ? a.x[b * T * D + k] : 0.f) : a.S.p[5][b * rs + (k - SR_DP)];
+    put_a(1, row, k, k < XK ? (k < D ? a.x[b * T * D + k] : 0.f) : a.S.p[5][b * rs + (k - XK)]);
   }
   __syncthreads();
 
   if (wave < 4) {
     // ------------------------------------------------------------------ producer (gate q)
-    // The B stream of a wave is the cyclic sequence of its GT = NT*KG groups per t (4 float4
-    // per lane each).  The loop walks it U groups at a time with a U-deep register ring:
-    // slot u holds group G+u and is refilled with group G+u+U right after its 16 MFMAs.
+    // The B stream of a wave is the cyclic sequence of its GT chunks per t (3 x 16 B per lane
+    // each).  The loop walks it U chunks at a time with a U-deep register ring: slot u holds
+    // chunk G+u and is refilled with chunk G+u+U right after its 6 MFMAs.
+    constexpr int GT = SG::GT, U = SG::U;
     const int q = wave, c = lane & 31, kh = lane >> 5;
-    const float4* wq = reinterpret_cast<const float4*>(wt) + (size_t)q * NT * KG * 4 * 64 + lane;
-    constexpr int GT = NT * KG;
-    constexpr int U = (GT % SR_PF == 0) ? SR_PF : ((GT % 3 == 0) ? 3 : 2);
-    static_assert(GT % U == 0, "group ring must divide the groups of a t");
-    float4 bq[U][4];
+    const bf16x8* wq = wt + (size_t)q * GT * 3 * 64 + lane;
+    bf16x8 bq[U][3];
 #pragma unroll
     for (int u = 0; u < U; ++u)
 #pragma unroll
-      for (int i = 0; i < 4; ++i) bq[u][i] = wq[(u * 4 + i) * 64];
+      for (int p = 0; p < 3; ++p) bq[u][p] = wq[(u * 3 + p) * 64];
     f32x16 acc = {};
     for (int t = 1; t <= T; ++t) {
-      const float* A = &Ab[t & 1][c * AS + 4 * kh];
+      const __bf16* A = &Ab[t & 1][c * AST + 8 * kh];
 #pragma unroll 1
       for (int G0 = 0; G0 < GT; G0 += U) {
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-          const int G = G0 + u, n = G / KG, gg = G - n * KG;
-          if (n == 0 && gg == KG - 1) __syncthreads();   // mid-step: h_{t-1} of tile NT-1 is in
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const float4 a4 = *reinterpret_cast<const float4*>(A + 32 * gg + 8 * i);
-            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a4.x, bq[u][i].x, acc, 0, 0, 0);
-            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a4.y, bq[u][i].y, acc, 0, 0, 0);
-            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a4.z, bq[u][i].z, acc, 0, 0, 0);
-            acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a4.w, bq[u][i].w, acc, 0, 0, 0);
-          }
+          const int G = G0 + u, n = G / KC2, cc = G - n * KC2;
+          if (n == 0 && cc == KC2 - 2) SR_SYNC();   // mid-step: h_{t-1} of tile NT-1 is in
+          const bf16x8 a0 = *reinterpret_cast<const bf16x8*>(A + 16 * cc);
+          const bf16x8 a1 = *reinterpret_cast<const bf16x8*>(A + AP + 16 * cc);
+          const bf16x8 a2 = *reinterpret_cast<const bf16x8*>(A + 2 * AP + 16 * cc);
+          // smallest terms first
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a2, bq[u][0], acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, bq[u][1], acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, bq[u][2], acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, bq[u][0], acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, bq[u][1], acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, bq[u][0], acc, 0, 0, 0);
           const int Gn = G + U < GT ? G + U : G + U - GT;
 #pragma unroll
-          for (int i = 0; i < 4; ++i) bq[u][i] = wq[(Gn * 4 + i) * 64];
-          if (gg == KG - 1) {
+          for (int p = 0; p < 3; ++p) bq[u][p] = wq[(Gn * 3 + p) * 64];
+          if (cc == KC2 - 1) {
             float* Z = &Zb[((t - 1) * NT + n) & 1][q * SR_ROWS * 32 + c];
 #pragma unroll
             for (int r = 0; r < 16; ++r) Z[acc_row(r, lane) * 32] = acc[r];
             acc = f32x16{};
-            __syncthreads();   // end of step
+            SR_SYNC();   // end of step
           }
         }
       }
     }
     __syncthreads();         // final step: the consumer drains the last tile
+#ifdef SR_TIMING
+    if (threadIdx.x == 0) { g_sr_wait[blockIdx.x][0] = sr_wait; g_sr_wait[blockIdx.x][1] = clock64() - sr_t0; }
+#endif
     return;
   }
 
   // -------------------------------------------------------------------- consumer
-  // Plane accesses go through buffer descriptors: one 32-bit byte offset per point serves
-  // every plane (no 64-bit address per plane and point), and the descriptor's record count
-  // (rows < r1) turns loads past the last row into zeros and drops their stores.
+  // Thread ct owns row ct/8 and hidden units 4(ct%8) .. +3 of every tile: each plane access is
+  // one 16-byte buffer op per lane (a wave: 8 rows x 128 B), so a tile costs a lane 11 loads
+  // and 15 stores -- with one load per point it was 100 memory ops, past the 63 a wave can have
+  // outstanding, and every tile waited out full memory round trips.  Plane accesses go through
+  // buffer descriptors: one 32-bit byte offset per thread serves every plane, and the record
+  // count (rows < r1) turns loads past the last row into zeros and drops their stores.
   const int ct = threadIdx.x - 4 * 64;      // 0..255
-  const int jl = ct & 31, rb = ct >> 5;      // rows rb + 8r, r = 0..3
+  const int row = ct >> 3, j4 = (ct & 7) * 4;
   const uint32_t pbytes = (uint32_t)(a.r1 * rs * 4), zbytes = (uint32_t)(a.r1 * T * H * 4);
   __amdgpu_buffer_rsrc_t rS[6], rL[6], rZ[4];
 #pragma unroll
@@ -372,82 +403,101 @@ __global__ __launch_bounds__(SR_THREADS) void k_sweep_rows(Geom g, const float* 
   }
 #pragma unroll
   for (int q = 0; q < 4; ++q) rZ[q] = __builtin_amdgcn_make_buffer_rsrc(a.zc + q * BTH, 0, zbytes, kBufWord3);
-  uint32_t pofs[4], zofs[4];                 // byte offsets of the points at t = 0 / t = 1, tile 0
-#pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const int64_t b = m0 + rb + 8 * r;
-    pofs[r] = (uint32_t)((b * rs + jl) * 4);
-    zofs[r] = (uint32_t)((b * T * H + jl) * 4);
-  }
-  // c_{t-1} of the consumer's points, by tile: Cs[n*4 + r][ct]
-  for (int n = 0; n < NT; ++n)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) Cs[n * 4 + r][ct] = buf_ld<0>(rS[4], pofs[r] + 128 * n);   // c_0
+  const uint32_t pofs = (uint32_t)(((m0 + row) * rs + j4) * 4);       // t = 0, tile 0
+  const uint32_t zofs = (uint32_t)(((m0 + row) * T * H + j4) * 4);    // t = 1, tile 0
 
-  auto load_tile = [&](int t, int n, SrState (&v)[4]) {
-    const uint32_t d = (uint32_t)(t * H + 32 * n) * 4;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const uint32_t o = pofs[r] + d;
-      v[r].f0 = buf_ld(rS[1], o); v[r].g0 = buf_ld(rS[2], o); v[r].c0 = buf_ld(rS[4], o); v[r].h0 = buf_ld(rS[5], o);
-      v[r].li = buf_ld(rL[0], o); v[r].lf = buf_ld(rL[1], o); v[r].lg = buf_ld(rL[2], o);
-      v[r].lo = buf_ld(rL[3], o); v[r].lc = buf_ld(rL[4], o); v[r].lh = buf_ld(rL[5], o);
-    }
+  struct St4 { f32x4 f0, g0, c0, h0, cp, li, lf, lg, lo, lc, lh; };
+  auto load_tile = [&](int t, int n, St4& v) {
+    const uint32_t o = pofs + (uint32_t)(t * H + 32 * n) * 4;
+    v.f0 = buf_ld4(rS[1], o); v.g0 = buf_ld4(rS[2], o); v.c0 = buf_ld4(rS[4], o); v.h0 = buf_ld4(rS[5], o);
+    v.cp = buf_ld4<0>(rS[4], o - H * 4);     // c_{t-1}, stored by this thread one t earlier
+    v.li = buf_ld4(rL[0], o); v.lf = buf_ld4(rL[1], o); v.lg = buf_ld4(rL[2], o);
+    v.lo = buf_ld4(rL[3], o); v.lc = buf_ld4(rL[4], o); v.lh = buf_ld4(rL[5], o);
   };
-  // x_{tn} into A-buffer tn&1 (32 rows x 32, four values per consumer thread)
+  // x_{tn} into A-buffer tn&1 (32 rows x XK)
   auto load_x = [&](int tn) {
     if (tn > T) return;
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int i = ct + 256 * u, row = i >> 5, k = i & 31;
-      const int64_t b = min(m0 + row, a.r1 - 1);
-      Ab[tn & 1][row * AS + k] = k < D ? a.x[(b * T + (tn - 1)) * D + k] : 0.f;
+    for (int u = 0; u < 2 * XC; ++u) {
+      const int i = ct + 256 * u, xr = i / XK, k = i % XK;
+      const int64_t b = min(m0 + xr, a.r1 - 1);
+      put_a(tn & 1, xr, k, k < D ? a.x[(b * T + (tn - 1)) * D + k] : 0.f);
     }
   };
 
-  SrState nxt[4];
+  St4 nxt;
   load_tile(1, 0, nxt);
   load_x(2);                 // step 0: the producer computes tile (1, 0)
   __syncthreads();           // its mid-step barrier
   __syncthreads();           // end of step 0
   for (int t = 1; t <= T; ++t) {
     const bool last = (t == T);
-    float* An = &Ab[(t + 1) & 1][SR_DP + jl];
+    __bf16* An = &Ab[(t + 1) & 1][row * AST + XK + j4];
 #pragma unroll 1
     for (int n = 0; n < NT; ++n) {
-      SrState cur[4];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) cur[r] = nxt[r];
+#ifdef SR_TIMING
+      const unsigned long long ta_ = clock64();
+#endif
+      const St4 cur = nxt;
+#ifdef SR_TIMING
+      asm volatile("" :: "v"(cur.f0), "v"(cur.g0), "v"(cur.c0), "v"(cur.h0), "v"(cur.li), "v"(cur.lf), "v"(cur.lg),
+                   "v"(cur.lo), "v"(cur.lc), "v"(cur.lh), "v"(cur.cp));
+      const unsigned long long tw_ = clock64();
+      if ((threadIdx.x & 63) == 0) sr_lw += tw_ - ta_;
+#endif
       if (n + 1 < NT) load_tile(t, n + 1, nxt);
       else if (!last) load_tile(t + 1, 0, nxt);
-      const float* Z = &Zb[((t - 1) * NT + n) & 1][(rb * 32) + jl];
-      const uint32_t d = (uint32_t)(t * H + 32 * n) * 4, dz = (uint32_t)((t - 1) * H + 32 * n) * 4;
+      const f32x4* Z = reinterpret_cast<const f32x4*>(&Zb[((t - 1) * NT + n) & 1][row * 32 + j4]);
+      const f32x4 zi = Z[0], zf = Z[SR_ROWS * 8], zg = Z[2 * SR_ROWS * 8], zo = Z[3 * SR_ROWS * 8];
+      f32x4 i1, f1, g1, o1, c1, h1, li, lf, lg, lo, lc;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
+      for (int u = 0; u < 4; ++u) {
         SweepIn v;
-        v.zi = Z[(8 * r) * 32]; v.zf = Z[SR_ROWS * 32 + (8 * r) * 32];
-        v.zg = Z[2 * SR_ROWS * 32 + (8 * r) * 32]; v.zo = Z[3 * SR_ROWS * 32 + (8 * r) * 32];
-        float* cp = &Cs[n * 4 + r][ct];
-        v.f0 = cur[r].f0; v.g0 = cur[r].g0; v.c0 = cur[r].c0; v.h0 = cur[r].h0; v.cp = *cp;
-        v.li = cur[r].li; v.lf = cur[r].lf; v.lg = cur[r].lg; v.lo = cur[r].lo; v.lc = cur[r].lc; v.lh = cur[r].lh;
+        v.zi = zi[u]; v.zf = zf[u]; v.zg = zg[u]; v.zo = zo[u];
+        v.f0 = cur.f0[u]; v.g0 = cur.g0[u]; v.c0 = cur.c0[u]; v.h0 = cur.h0[u]; v.cp = cur.cp[u];
+        v.li = cur.li[u]; v.lf = cur.lf[u]; v.lg = cur.lg[u]; v.lo = cur.lo[u]; v.lc = cur.lc[u]; v.lh = cur.lh[u];
         const SweepRes o = sweep_point(hp, v, last);
-        *cp = o.c1;
-        if (!last) An[(rb + 8 * r) * AS + 32 * n] = o.h1;
-        const uint32_t po = pofs[r] + d, zo = zofs[r] + dz;
-        buf_st(rS[0], po, o.i1); buf_st(rS[1], po, o.f1); buf_st(rS[2], po, o.g1); buf_st(rS[3], po, o.o1);
-        buf_st<0>(rS[4], po, o.c1);          // c_t and h_t are read back by the next step's kernels
-        if (!last) buf_st<0>(rS[5], po, o.h1);
-        buf_st(rL[0], po, o.li); buf_st(rL[1], po, o.lf); buf_st(rL[2], po, o.lg); buf_st(rL[3], po, o.lo);
-        buf_st(rL[4], po, o.lc);
-        buf_st(rZ[0], zo, v.zi); buf_st(rZ[1], zo, v.zf); buf_st(rZ[2], zo, v.zg); buf_st(rZ[3], zo, v.zo);
+        i1[u] = o.i1; f1[u] = o.f1; g1[u] = o.g1; o1[u] = o.o1; c1[u] = o.c1; h1[u] = o.h1;
+        li[u] = o.li; lf[u] = o.lf; lg[u] = o.lg; lo[u] = o.lo; lc[u] = o.lc;
       }
+#ifdef SR_TIMING
+      asm volatile("" :: "v"(i1), "v"(f1), "v"(g1), "v"(o1), "v"(c1), "v"(h1), "v"(li), "v"(lf), "v"(lg), "v"(lo), "v"(lc));
+      const unsigned long long tb_ = clock64();
+#endif
+      if (!last) {
+        bf16x4 p0, p1, p2;
+        split3(h1, p0, p1, p2);
+        __bf16* d = An + 32 * n;
+        *reinterpret_cast<bf16x4*>(d) = p0;
+        *reinterpret_cast<bf16x4*>(d + AP) = p1;
+        *reinterpret_cast<bf16x4*>(d + 2 * AP) = p2;
+      }
+      const uint32_t po = pofs + (uint32_t)(t * H + 32 * n) * 4, zo4 = zofs + (uint32_t)((t - 1) * H + 32 * n) * 4;
+      buf_st4(rS[0], po, i1); buf_st4(rS[1], po, f1); buf_st4(rS[2], po, g1); buf_st4(rS[3], po, o1);
+      buf_st4<0>(rS[4], po, c1);             // c_t: read back at t+1 (here) and by the next step's kernels
+      if (!last) buf_st4<0>(rS[5], po, h1);
+      buf_st4(rL[0], po, li); buf_st4(rL[1], po, lf); buf_st4(rL[2], po, lg); buf_st4(rL[3], po, lo);
+      buf_st4(rL[4], po, lc);
+      buf_st4(rZ[0], zo4, zi); buf_st4(rZ[1], zo4, zf); buf_st4(rZ[2], zo4, zg); buf_st4(rZ[3], zo4, zo);
+#ifdef SR_TIMING
+      const unsigned long long tc_ = clock64();
+      if ((threadIdx.x & 63) == 0) { sr_comp += tb_ - ta_; sr_store += tc_ - tb_; }
+#endif
       if (n == NT - 1 && !last) {
         load_x(t + 2);       // the producer's next tile is (t+1, 0)
-        __syncthreads();     // its mid-step barrier: h_t is complete
+        SR_SYNC();           // its mid-step barrier: h_t is complete
       }
-      __syncthreads();       // end of step
+      SR_SYNC();             // end of step
     }
   }
+#ifdef SR_TIMING
+  if (threadIdx.x == 256) {
+    g_sr_wait[1024 + blockIdx.x][0] = sr_wait;
+    g_sr_wait[1024 + blockIdx.x][1] = sr_comp;
+    g_sr_wait[1536 + blockIdx.x][0] = sr_store;
+    g_sr_wait[1536 + blockIdx.x][1] = sr_lw;
+  }
+#endif
 }
 
 __global__ __launch_bounds__(kThreads) void k_rowdot(int64_t B, int H, int O, const float* h, int64_t hs,
@@ -1665,24 +1715,36 @@ void launch_sweep_t(const Geom& g, int t, const Weights& w, const Hyper& hp, con
 
 bool sweep_rows_ok(const Geom& g) {
   // 32-bit buffer offsets: a [B][T+1][H] plane and a [B*T][H] z-cache plane in bytes
-  return g.H % 32 == 0 && g.H <= 256 && g.D <= SR_DP && g.B * (int64_t)g.TP() * g.H * 4 < (int64_t)UINT32_MAX;
+  return g.H % 32 == 0 && g.H <= 256 && g.D <= 32 && g.B * (int64_t)g.TP() * g.H * 4 < (int64_t)UINT32_MAX;
 }
 
-size_t sweep_wt_floats(const Geom& g) { return (size_t)4 * (g.H / 32) * ((SR_DP + g.H) / 8) * 256; }
+static int sweep_xc(const Geom& g) { return (g.D + 15) / 16; }
+
+size_t sweep_wt_floats(const Geom& g) {   // bf16x8 image, in float units
+  return (size_t)4 * (g.H / 32) * (sweep_xc(g) + 2 * (g.H / 32)) * 3 * 64 * 4;
+}
 
 void launch_sweep_wt(const Geom& g, const Weights& w, float* wt, hipStream_t s) {
-  const int total = 4 * (g.H / 32) * ((SR_DP + g.H) / 8) * 64;
-  k_sweep_wt<<<cdiv64(total, kThreads), kThreads, 0, s>>>(g.D, g.H, w, wt);
+  const int xc = sweep_xc(g), NT = g.H / 32;
+  const int total = 4 * NT * (xc + 2 * NT) * 64;
+  k_sweep_wt<<<cdiv64(total, kThreads), kThreads, 0, s>>>(g.D, g.H, xc, w, reinterpret_cast<bf16x8*>(wt));
 }
 
-void launch_sweep_rows(const Geom& g, const float* wt, const Hyper& hp, const SweepT& a, hipStream_t s) {
+template <int XC>
+static void launch_sweep_rows_xc(const Geom& g, const bf16x8* wt, const Hyper& hp, const SweepT& a, hipStream_t s) {
   dim3 grid(cdiv64(a.r1 - a.r0, SR_ROWS));
   switch (g.H / 32) {
-#define SR_CASE(N) case N: k_sweep_rows<N><<<grid, SR_THREADS, 0, s>>>(g, wt, hp, a); break;
+#define SR_CASE(N) case N: k_sweep_rows<N, XC><<<grid, SR_THREADS, 0, s>>>(g, wt, hp, a); break;
     SR_CASE(1) SR_CASE(2) SR_CASE(3) SR_CASE(4) SR_CASE(5) SR_CASE(6) SR_CASE(7) SR_CASE(8)
 #undef SR_CASE
     default: break;
   }
+}
+
+void launch_sweep_rows(const Geom& g, const float* wt, const Hyper& hp, const SweepT& a, hipStream_t s) {
+  const bf16x8* w = reinterpret_cast<const bf16x8*>(wt);
+  if (sweep_xc(g) == 1) launch_sweep_rows_xc<1>(g, w, hp, a, s);
+  else launch_sweep_rows_xc<2>(g, w, hp, a, s);
 }
 
 void launch_rowdot(int64_t B, int H, int O, const float* h, int64_t hs, const float* wy, float* out, hipStream_t s) {
@@ -1893,3 +1955,17 @@ void launch_ht_apply(const Geom& g, const Hyper& hp, const Planes6& S, const Pla
 }
 
 }  // namespace admm
+
+#ifdef SR_TIMING
+extern "C" void sr_timing_dump(int nblk) {
+  unsigned long long h[2048][2];
+  (void)hipMemcpyFromSymbol(h, HIP_SYMBOL(admm::g_sr_wait), sizeof(h));
+  double pw = 0, cw = 0, tot = 0, cc = 0, cs = 0, lw = 0;
+  for (int b = 0; b < nblk; ++b) {
+    pw += h[b][0]; tot += h[b][1]; cw += h[1024 + b][0]; cc += h[1024 + b][1]; cs += h[1536 + b][0]; lw += h[1536 + b][1];
+  }
+  printf("sweep rows timing: total %.0f cyc/WG, producer waits %.1f%%, consumer waits %.1f%%, "
+         "consumer load+compute %.1f%% (load wait %.1f%%), consumer store issue %.1f%%\n", tot / nblk,
+         100.0 * pw / tot, 100.0 * cw / tot, 100.0 * cc / tot, 100.0 * lw / tot, 100.0 * cs / tot);
+}
+#endif

@@ -35,6 +35,11 @@ import torch  # noqa: E402
 
 PEAK_FP32_MFMA = 157.3e12   # MI355X_MICROARCH.md: Peak FP32 (matrix) 157.3 TFLOPS
 PEAK_HBM = 8.0e12           # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+PEAK_BF16_MFMA = 2.5e15     # MI355X_MICROARCH.md: BF16 ~2.5 PF dense
+# f32-accurate products from three-way bf16 splits take 6 bf16 MFMAs (admm_dev.hpp split3):
+# the matrix peak of the kernels that use them, in f32-equivalent flops
+PEAK_SPLIT3_MFMA = PEAK_BF16_MFMA / 6
+SPLIT3_CLASSES = ('sweep',)
 HEADLINE_B = 8192
 
 CONFIGS = {
@@ -63,7 +68,8 @@ def roofline_terms(cls: str, B: int, T: int, D: int, H: int):
     """Algorithmic (flops, bytes) of ONE launch of a kernel class."""
     f4 = 4  # bytes per fp32
     if cls == 'sweep':            # whole sweep t = 1..T: per t [B, D+H] x [D+H, 4H] + fused gate/dual updates
-        return T * 2.0 * B * (D + H) * 4 * H, T * f4 * B * (D + 27 * H)
+        # per (b, t, j): 11 state/dual loads (incl. c_{t-1}), 15 stores (6 gates, 5 duals, 4 z)
+        return T * 2.0 * B * (D + H) * 4 * H, T * f4 * B * (D + 26 * H)
     n = float(B) * T * H          # elements of one [B*T, H] plane
     if cls == 'atr_h':            # G_q = Hprev^T R_q, 4 gates
         return 2.0 * B * T * H * 4 * H, f4 * (B * T * H + 4 * n)
@@ -81,7 +87,7 @@ def roofline_terms(cls: str, B: int, T: int, D: int, H: int):
 
 
 # kernel symbols of each profile class (admm_kernels.hip), for the committed PMC traffic
-CLASS_KERNELS = {'sweep': ('k_sweep_t',), 'atr_h': ('k_atr_fused', 'k_atr<128'), 'qgemm_h': ('k_qgemm<true, 1>',),
+CLASS_KERNELS = {'sweep': ('k_sweep_rows', 'k_sweep_t'), 'atr_h': ('k_atr_fused', 'k_atr<128'), 'qgemm_h': ('k_qgemm<true, 1>',),
                  'trial': ('k_trial_fast', 'k_trial<'), 'resid': ('k_resid_gx', 'k_apply_dwx', 'k_resid<')}
 
 
@@ -97,12 +103,15 @@ def pmc_traffic(cls: str, cfg_name: str):
     kern = json.load(open(files[-1]))['kernels']
     # trial passes after the first return early (gates already decided): use the full pass
     key = 'traffic_bytes_max' if cls == 'trial' else 'traffic_bytes_median'
-    vals = [v[key] for k, v in kern.items() if k.startswith(CLASS_KERNELS[cls])]
+    for prefix in CLASS_KERNELS[cls]:     # the first kernel family present in the profile
+        vals = [v[key] for k, v in kern.items() if k.startswith(prefix)]
+        if vals:
+            break
     if not vals:
         return None
     per = sum(vals) / len(vals)
-    if cls == 'sweep':   # one class launch = T time steps x 2 sample halves
-        _, T = CONFIGS[cfg_name][0], CONFIGS[cfg_name][1]
+    if cls == 'sweep' and prefix == 'k_sweep_t':   # per-t sweep: T time steps x 2 sample halves
+        T = CONFIGS[cfg_name][1]
         per *= 2 * T
     return per
 
@@ -223,9 +232,10 @@ def main():
         n = prof[cls][1]
         avg_s = ms / n / 1e3
         flops, nbytes = roofline_terms(cls, per, T, D, H)
-        t_mfma, t_hbm = flops / PEAK_FP32_MFMA, nbytes / PEAK_HBM
+        peak_mfma = PEAK_SPLIT3_MFMA if cls in SPLIT3_CLASSES else PEAK_FP32_MFMA
+        t_mfma, t_hbm = flops / peak_mfma, nbytes / PEAK_HBM
         if t_mfma >= t_hbm:
-            roof = {'bound': 'mfma', 'achieved': flops / avg_s / 1e12, 'peak': PEAK_FP32_MFMA / 1e12,
+            roof = {'bound': 'mfma', 'achieved': flops / avg_s / 1e12, 'peak': peak_mfma / 1e12,
                     'unit': 'TFLOP/s'}
         else:
             roof = {'bound': 'hbm', 'achieved': nbytes / avg_s / 1e9, 'peak': PEAK_HBM / 1e9, 'unit': 'GB/s'}

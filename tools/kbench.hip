@@ -21,6 +21,9 @@ static float* dev_random(size_t n, float lo, float hi, unsigned seed) {
   return d;
 }
 
+#ifdef SR_TIMING
+extern "C" void sr_timing_dump(int nblk);
+#endif
 static void timeit(const char* name, double bytes, double flops, const std::function<void()>& f) {
   hipEvent_t a, b;
   (void)hipEventCreate(&a); (void)hipEventCreate(&b);
@@ -100,6 +103,10 @@ int main(int argc, char** argv) {
       float* wt; (void)hipMalloc(&wt, sweep_wt_floats(g) * 4);
       timeit("sweep_wt", 0, 0, [&] { launch_sweep_wt(g, w, wt, s); });
       timeit("sweep rows (1 launch)", sb, sf, [&] { launch_sweep_rows(g, wt, hp, sw, s); });
+#ifdef SR_TIMING
+      (void)hipDeviceSynchronize();
+      sr_timing_dump((int)((g.B + 31) / 32));
+#endif
     }
     timeit("sweep T steps, 2 streams", sb, sf, [&] {
       const int64_t mid = (g.B / 2 + 127) / 128 * 128;

@@ -53,20 +53,19 @@ __device__ __forceinline__ float sigm(float z) { return sig_pair(z).s; }
 
 __device__ __forceinline__ float act(bool is_tanh, float z) { return is_tanh ? tanhf(z) : sigm(z); }
 
-// expm1(x) to ~1 ulp: degree-8 Taylor on |x| < 1/2 (truncation < 2^-26 relative), else exp - 1
+// expm1(x) to ~1 ulp: degree-8 Taylor on |x| < 1/2 (truncation < 2^-26 relative), else exp - 1.
+// Branch-free (both forms, then a select): a per-lane branch here costs more than the 9 FMAs.
 __device__ __forceinline__ float expm1_acc(float x) {
-  if (fabsf(x) < 0.5f) {
-    float p = 1.f / 40320.f;
-    p = fmaf(p, x, 1.f / 5040.f);
-    p = fmaf(p, x, 1.f / 720.f);
-    p = fmaf(p, x, 1.f / 120.f);
-    p = fmaf(p, x, 1.f / 24.f);
-    p = fmaf(p, x, 1.f / 6.f);
-    p = fmaf(p, x, 0.5f);
-    p = fmaf(p, x, 1.f);
-    return p * x;
-  }
-  return __expf(x) - 1.f;
+  float p = 1.f / 40320.f;
+  p = fmaf(p, x, 1.f / 5040.f);
+  p = fmaf(p, x, 1.f / 720.f);
+  p = fmaf(p, x, 1.f / 120.f);
+  p = fmaf(p, x, 1.f / 24.f);
+  p = fmaf(p, x, 1.f / 6.f);
+  p = fmaf(p, x, 0.5f);
+  p = fmaf(p, x, 1.f);
+  const float e = __expf(x) - 1.f;
+  return fabsf(x) < 0.5f ? p * x : e;
 }
 
 // Three-way bf16 split of f32 values: a = p0 + p1 + p2 to ~2^-27 relative (each remainder is

@@ -77,6 +77,8 @@ struct AdmmCtx {
   int sweep_split = 2;     // sample parts of the sweep, one stream each (ADMM_SWEEP_SPLIT)
   bool sweep_rows = false; // whole sweep as one persistent launch (k_sweep_rows; ADMM_SWEEP_ROWS=0 disables)
   float* swt = nullptr;    // its B-operand image of the weights
+  bool split3 = false;     // h-stage GEMMs on split bf16 MFMAs (admm_split3.hip; ADMM_SPLIT3=0 disables)
+  float* gimg = nullptr;   // split image of G_h for k_qgemm3
   hipStream_t sx[kMaxSweepStreams - 1] = {};
   hipEvent_t ev_fork = nullptr, ev_join[kMaxSweepStreams - 1] = {};
   float *U = nullptr, *wy_slab = nullptr, *Gy = nullptr;
@@ -188,6 +190,10 @@ int stage_weights(AdmmCtx* c, int side, hipStream_t s) {
     ns = c->nblk_rx;
     ProfScope ps(c, ADMM_PROF_RESID, s);
     launch_resid_gx(g, c->hp, c->buf.x, S, L, c->zc, c->tgt, c->gslab, ns, s);
+  } else if (fast && c->split3) {
+    ns = atr3_splits(g);
+    ProfScope ps(c, ADMM_PROF_ATR_H, s);
+    launch_atr3(g, c->buf.gates[ADMM_H], c->zc, c->tgt, c->gslab, ns, s);
   } else if (fast) {
     ns = atr_splits(g, 1);
     ProfScope ps(c, ADMM_PROF_ATR_H, s);
@@ -217,7 +223,8 @@ int stage_weights(AdmmCtx* c, int side, hipStream_t s) {
   // 2. trial direction Q = A G (not needed on the fast x side: formed inside the trials)
   if (!(fast && side == 0)) {
     ProfScope ps(c, side == 0 ? ADMM_PROF_QGEMM_X : ADMM_PROF_QGEMM_H, s);
-    launch_qgemm(g, side, c->buf.x, c->buf.gates[ADMM_H], c->G, c->Q, s);
+    if (side == 1 && c->split3) launch_qgemm3(g, c->buf.gates[ADMM_H], c->G, c->gimg, c->Q, s);
+    else launch_qgemm(g, side, c->buf.x, c->buf.gates[ADMM_H], c->G, c->Q, s);
   }
   // 3. line search: trial passes of kTrialJ exponents each until every gate has passed
   SelectArgs sa{};
@@ -350,6 +357,8 @@ int admm_create(const AdmmDims* dims, const AdmmParams* params, int device, Admm
     c->sweep_split = std::max(1, std::min(kMaxSweepStreams, std::atoi(e)));
   c->sweep_rows = sweep_rows_ok(g);
   if (const char* e = std::getenv("ADMM_SWEEP_ROWS")) c->sweep_rows = c->sweep_rows && std::atoi(e) != 0;
+  c->split3 = fast_path(g) && split3_ok(g);
+  if (const char* e = std::getenv("ADMM_SPLIT3")) c->split3 = c->split3 && std::atoi(e) != 0;
   Hyper& h = c->hp;
   for (int i = 0; i < 7; ++i) h.rho[i] = params->rho[i];
   for (int q = 0; q < 4; ++q) {
@@ -368,6 +377,7 @@ int admm_create(const AdmmDims* dims, const AdmmParams* params, int device, Admm
   size_t slab = (size_t)atr_splits(g, 0) * 4 * g.D * g.H;
   slab = std::max(slab, (size_t)atr_splits(g, 1) * 4 * g.H * g.H);
   slab = std::max(slab, (size_t)c->nblk_rx * 4 * g.D * g.H);
+  if (c->split3) slab = std::max(slab, (size_t)atr3_splits(g) * 4 * g.H * g.H);
   c->wy_nsplit = wy_splits(g);
   c->ht_nblk = ht_blocks(g);
   if ((rc = dalloc(&c->zc, 4 * plane)) || (rc = dalloc(&c->tgt, 4 * plane)) || (rc = dalloc(&c->R, fast_path(g) ? 1 : 4 * plane)) ||
@@ -380,7 +390,8 @@ int admm_create(const AdmmDims* dims, const AdmmParams* params, int device, Admm
       (rc = dalloc(&c->U, (size_t)g.B * g.O)) || (rc = dalloc(&c->wy_slab, (size_t)c->wy_nsplit * g.H * g.O)) ||
       (rc = dalloc(&c->Gy, (size_t)g.H * g.O)) || (rc = dalloc(&c->ht_part, (size_t)c->ht_nblk * kHTSums)) ||
       (rc = dalloc(&c->ht_sums, kHTSums)) || (rc = dalloc(&c->stats, 1)) ||
-      (c->sweep_rows && (rc = dalloc(&c->swt, sweep_wt_floats(g))))) {
+      (c->sweep_rows && (rc = dalloc(&c->swt, sweep_wt_floats(g)))) ||
+      (c->split3 && (rc = dalloc(&c->gimg, split3_gimg_floats(g))))) {
     std::string msg = g_last_error;
     admm_destroy(c);
     return fail(rc, "%s", msg.c_str());
@@ -405,7 +416,7 @@ int admm_destroy(AdmmCtx* c) {
   if (!c) return ADMM_OK;
   (void)hipSetDevice(c->device);
   void* ptrs[] = {c->zc, c->tgt, c->R, c->Q, c->G, c->dW, c->gslab, c->tr_part, c->tr_sums, c->tr_poly, c->found, c->pick,
-                  c->U, c->wy_slab, c->Gy, c->ht_part, c->ht_sums, c->stats, c->swt};
+                  c->U, c->wy_slab, c->Gy, c->ht_part, c->ht_sums, c->stats, c->swt, c->gimg};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   if (c->comm) ncclCommDestroy(c->comm);

@@ -156,6 +156,15 @@ void launch_apply_dwx(const Geom& g, const float* x, const float* dW, float* zc,
 // h stage A^T R with R computed on the fly from zc (already updated) and tgt (side 1, fast path)
 void launch_atr_fused(const Geom& g, const Hyper& hp, const float* x, const float* Sh, const float* zc,
                       const float* tgt, const float* dW, float* slab, int nsplit, hipStream_t s);
+// h stage on bf16 matrix cores with three-way split f32 operands (admm_split3.hip), H % 256 == 0:
+// slab[sp][q][m][j] = sum_rows Hprev[row][m] R_q[row][j] (R from zc, tgt), and Q = Hprev G
+// (gimg: split3_gimg_floats(g) floats of workspace for the split G image)
+bool split3_ok(const Geom& g);
+size_t split3_gimg_floats(const Geom& g);
+int atr3_splits(const Geom& g);
+void launch_atr3(const Geom& g, const float* Sh, const float* zc, const float* tgt, float* slab, int nsplit,
+                 hipStream_t s);
+void launch_qgemm3(const Geom& g, const float* Sh, const float* G, float* gimg, float* Q, hipStream_t s);
 // decide the first passing k in this pass's window; on success update the weights
 struct SelectArgs {
   int side;                 // 0 x, 1 h

@@ -39,7 +39,7 @@ PEAK_BF16_MFMA = 2.5e15     # MI355X_MICROARCH.md: BF16 ~2.5 PF dense
 # f32-accurate products from three-way bf16 splits take 6 bf16 MFMAs (admm_dev.hpp split3):
 # the matrix peak of the kernels that use them, in f32-equivalent flops
 PEAK_SPLIT3_MFMA = PEAK_BF16_MFMA / 6
-SPLIT3_CLASSES = ('sweep',)
+SPLIT3_CLASSES = ('sweep', 'atr_h', 'qgemm_h')
 HEADLINE_B = 8192
 
 CONFIGS = {
@@ -87,7 +87,7 @@ def roofline_terms(cls: str, B: int, T: int, D: int, H: int):
 
 
 # kernel symbols of each profile class (admm_kernels.hip), for the committed PMC traffic
-CLASS_KERNELS = {'sweep': ('k_sweep_rows', 'k_sweep_t'), 'atr_h': ('k_atr_fused', 'k_atr<128'), 'qgemm_h': ('k_qgemm<true, 1>',),
+CLASS_KERNELS = {'sweep': ('k_sweep_rows', 'k_sweep_t'), 'atr_h': ('k_atr3', 'k_atr_fused', 'k_atr<128'), 'qgemm_h': ('k_qgemm3', 'k_qgemm<true, 1>'),
                  'trial': ('k_trial_fast', 'k_trial<'), 'resid': ('k_resid_gx', 'k_apply_dwx', 'k_resid<')}
 
 

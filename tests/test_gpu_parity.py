@@ -403,3 +403,38 @@ def test_persistent_sweep_matches_per_t_sweep(mods, dev, monkeypatch):
         for q in GATES6:
             d = float((out['1'][k][q] - out['0'][k][q]).abs().max())
             assert d <= 1e-5, (k, q, d)
+
+
+def test_split3_h_stage_matches_f32_mfma(mods, dev, monkeypatch):
+    """The h-stage GEMMs on split bf16 MFMAs (admm_split3.hip, used when H % 256 == 0) agree
+    with the f32-MFMA kernels (ADMM_SPLIT3=0) on a C3-shaped problem (H = 256, D = 16) over
+    three steps: same line-search exponents, weights and state within 1e-5."""
+    from blocks.lstm import LSTM
+    from parameters import example_parameter_dictionary
+    admm, _ = mods
+    admm.with_dual_y = False
+    B, T, D, H = 500, 3, 16, 256
+    g = torch.Generator().manual_seed(12)
+    x = torch.rand(B, T, D, generator=g).to(dev)
+    y = (0.8 * x.mean((1, 2)).unsqueeze(1) + 0.1 * torch.rand(B, 1, generator=g).to(dev)).contiguous()
+    pd = example_parameter_dictionary['GoogleStock']
+    out = {}
+    for flag in ('1', '0'):
+        monkeypatch.setenv('ADMM_SPLIT3', flag)
+        torch.manual_seed(0)
+        m = LSTM(D, H, 1).to(dev)
+        opt = admm.ADMMBasedOptimizer(m, (x, y), pd, verbose=False)
+        ks = []
+        for _ in range(3):
+            opt.step()
+            ks.append(list(opt.last_step_stats()['k'].values()))
+        out[flag] = (ks, {n: p.detach().clone() for n, p in m.named_parameters()},
+                     {q: opt.gates[q].clone() for q in GATES6}, {q: opt.duals[q].clone() for q in GATES6})
+    assert out['1'][0] == out['0'][0]
+    for n in out['1'][1]:
+        a, b = out['1'][1][n], out['0'][1][n]
+        assert float((a - b).abs().max()) <= 1e-5 * max(1.0, float(b.abs().max())), n
+    for k in (2, 3):
+        for q in GATES6:
+            d = float((out['1'][k][q] - out['0'][k][q]).abs().max())
+            assert d <= 1e-5, (k, q, d)

@@ -6,6 +6,8 @@
 #include <functional>
 #include <random>
 #include <vector>
+#include <cmath>
+#include <algorithm>
 #include "../admm-lstm_amd/admm_amd/csrc/admm_kernels.hpp"
 
 using namespace admm;
@@ -66,6 +68,42 @@ int main(int argc, char** argv) {
   hipStream_t s = 0;
   const double f4 = 4.0;
   const int nb = stream_blocks(g);
+  auto run_s3 = [&] {
+  if (split3_ok(g)) {
+    // split-bf16 h-stage GEMMs: timing, and agreement with the f32-MFMA kernels above
+    const int ns3 = atr3_splits(g);
+    float* slab3; (void)hipMalloc(&slab3, (size_t)ns3 * 4 * g.H * g.H * 4);
+    float* gimg; (void)hipMalloc(&gimg, split3_gimg_floats(g) * 4);
+    float* Q3; (void)hipMalloc(&Q3, (size_t)4 * n * 4);
+    timeit("atr3 (split bf16)", f4 * (2 * 4 * n + BT * g.H), 2.0 * BT * g.H * 4 * g.H,
+           [&] { launch_atr3(g, S.p[5], zc, tgt, slab3, ns3, s); });
+    timeit("qgemm3 (split bf16)", f4 * (4 * n + BT * g.H), 2.0 * BT * g.H * 4 * g.H,
+           [&] { launch_qgemm3(g, S.p[5], G, gimg, Q3, s); });
+    launch_atr_fused(g, hp, x, S.p[5], zc, tgt, dW, slab, atr_splits(g, 1), s);
+    launch_qgemm(g, 1, x, S.p[5], G, Q, s);
+    (void)hipDeviceSynchronize();
+    const size_t gh = (size_t)4 * g.H * g.H;
+    const int ns = atr_splits(g, 1);
+    std::vector<float> a(ns * gh), b(ns3 * gh);
+    (void)hipMemcpy(a.data(), slab, a.size() * 4, hipMemcpyDeviceToHost);
+    (void)hipMemcpy(b.data(), slab3, b.size() * 4, hipMemcpyDeviceToHost);
+    double md = 0, mx = 0;
+    for (size_t i = 0; i < gh; ++i) {
+      double sa = 0, sb = 0;
+      for (int k = 0; k < ns; ++k) sa += a[k * gh + i];
+      for (int k = 0; k < ns3; ++k) sb += b[k * gh + i];
+      md = std::max(md, std::fabs(sa - sb)); mx = std::max(mx, std::fabs(sa));
+    }
+    printf("atr3 vs atr_fused: max |diff| %.3e (max |G| %.3e, rel %.2e)\n", md, mx, md / mx);
+    std::vector<float> qa(4 * n), qb(4 * n);
+    (void)hipMemcpy(qa.data(), Q, qa.size() * 4, hipMemcpyDeviceToHost);
+    (void)hipMemcpy(qb.data(), Q3, qb.size() * 4, hipMemcpyDeviceToHost);
+    md = 0; mx = 0;
+    for (size_t i = 0; i < qa.size(); ++i) { md = std::max(md, (double)std::fabs(qa[i] - qb[i])); mx = std::max(mx, (double)std::fabs(qa[i])); }
+    printf("qgemm3 vs qgemm: max |diff| %.3e (max |Q| %.3e, rel %.2e)\n", md, mx, md / mx);
+  }
+  };
+  if (argc > 2) { run_s3(); return 0; }
   timeit("apply_dwx", 2 * f4 * 4 * n + f4 * BT * g.D, 0, [&] { launch_apply_dwx(g, x, dW, zc, s); });
   timeit("trial_fast side0", f4 * 2 * 4 * n, 0, [&] { launch_trial_fast(g, 0, 0, zc, tgt, nullptr, x, G, found, part, nb, s); });
   timeit("trial_fast side1", f4 * 3 * 4 * n, 0, [&] { launch_trial_fast(g, 1, 0, zc, tgt, Q, x, dW, found, part, nb, s); });
@@ -86,6 +124,7 @@ int main(int argc, char** argv) {
   timeit("atr (R materialised)", f4 * (4 * n + BT * g.H), 2.0 * BT * g.H * 4 * g.H,
          [&] { launch_atr(g, 1, x, S.p[5], R, slab, ns, s); });
   timeit("qgemm side1", f4 * (4 * n + BT * g.H), 2.0 * BT * g.H * 4 * g.H, [&] { launch_qgemm(g, 1, x, S.p[5], G, Q, s); });
+  run_s3();
   SweepT sw{x, S, L, zc, 0, g.B};
   timeit("sweep_t (t=5)", f4 * g.B * (g.D + 27.0 * g.H), 2.0 * g.B * (g.D + g.H) * 4 * g.H,
          [&] { launch_sweep_t(g, 5, w, hp, sw, s); });

@@ -239,6 +239,8 @@ int stage_weights(AdmmCtx* c, int side, hipStream_t s) {
   sa.pick = c->pick;
   sa.stats = c->stats;
   const int nblk = fast ? stream_blocks(g) : c->nblk_trial;
+  // the row-pair trial kernel (H % 256 == 0) writes one partial per (block, column block)
+  const int nred = fast && trial_rows_ok(g) ? nblk * (g.H / 256) : nblk;
   for (int pass = 0; pass < kMaxPasses; ++pass) {
     {
       ProfScope ps(c, pass == 0 ? ADMM_PROF_TRIAL : ADMM_PROF_TRIAL_EXTRA, s);
@@ -248,7 +250,7 @@ int stage_weights(AdmmCtx* c, int side, hipStream_t s) {
       else
         launch_trial(g, pass, c->zc, c->tgt, c->Q, c->found, c->tr_part, nblk, s);
     }
-    launch_trial_reduce(g, pass, c->tr_part, nblk, c->found, c->tr_sums, s);
+    launch_trial_reduce(g, pass, c->tr_part, nred, c->found, c->tr_sums, s);
     rc = allreduce_f64(c, c->tr_sums, 4 * kTrialSlots, s);
     if (rc) return rc;
     sa.pass = pass;
@@ -372,7 +374,7 @@ int admm_create(const AdmmDims* dims, const AdmmParams* params, int device, Admm
   const size_t plane = (size_t)g.BT() * g.H;
   const int Kmax = g.D > g.H ? g.D : g.H;
   c->nblk_resid = resid_blocks(g);
-  c->nblk_trial = std::max(trial_blocks(g), stream_blocks(g));
+  c->nblk_trial = std::max(trial_blocks(g), stream_blocks(g) * (trial_rows_ok(g) ? g.H / 256 : 1));
   c->nblk_rx = resid_gx_blocks(g);
   size_t slab = (size_t)atr_splits(g, 0) * 4 * g.D * g.H;
   slab = std::max(slab, (size_t)atr_splits(g, 1) * 4 * g.H * g.H);

@@ -865,9 +865,9 @@ __global__ __launch_bounds__(kThreads) void k_qgemm(Geom g, const float* x, cons
 // Trial pass.  For the line search (admm.py:316-336) each gate needs, for k = 0, 1, ...,
 //   f(W + G/2^k) - f(W) = 0.5 rho sum_e [ (d0 + D_k)^2 - d0^2 ],  D_k = phi(z + q 2^-k) - phi(z),
 // evaluated without cancellation (DESIGN.md "line-search numerics").  Two regimes per element:
-//  * |q| <= 2^-8 (the common case): D_k = a1 s + a2 s^2 + a3 s^3 with s = 2^-k and
-//    a_n = c_n q^n (3-term Taylor, truncation < 1e-8 relative for every k >= 0), so the
-//    increment is a degree-6 polynomial in s whose 6 coefficients are summed once (pass 0)
+//  * |q| <= 2^-5 (the common case): D_k = sum_{n<=5} a_n s^n with s = 2^-k and a_n = c_n q^n
+//    (5-term Taylor: truncation |c6/c1| (qs)^5 <= 2e-8 relative to D for every k >= 0), so the
+//    increment is a degree-10 polynomial in s whose 10 coefficients are summed once (pass 0)
 //    and cover every exponent;
 //  * otherwise: D_k per candidate of the pass window k in [pass*J, pass*J + J), branch-free
 //    (see trial_direct).
@@ -907,7 +907,7 @@ __device__ __forceinline__ void direct_candidates(float cr, float e, float E, fl
 // five inputs are appended (ballot + prefix count) to an LDS ring of this wave, and the
 // loop runs once 64 entries are pending, with every lane busy.  All lanes of a wave must
 // make the same sequence of dq_push / dq_run calls (loops below are wave-uniform).
-constexpr int kDQ = 128;   // ring capacity: pending <= 63 before a push of <= 64
+constexpr int kDQ = 256;   // ring capacity: pending <= 63 before up to two pushes of <= 64 (trial_pair)
 struct DirectQ {
   float* buf;              // this wave's [5][kDQ] in LDS
   int head, tail;          // wave-uniform counters
@@ -929,9 +929,10 @@ __device__ __forceinline__ void dq_push(DirectQ& dq, bool p, float cr, float e, 
 
 __device__ __forceinline__ void dq_run(DirectQ& dq, float (&acc)[kSlots], bool final) {
   while (dq.tail - dq.head >= 64 || (final && dq.tail > dq.head)) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    // the queue is written and read by the lanes of one wave: LDS operations of a wave execute
+    // in order, so a wave barrier (no memory fence: a fence would make every global load of
+    // the caller's loop a clobbered, vector load) orders the pushes before these reads
     __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     const int lane = threadIdx.x & 63;
     const int n = dq.tail - dq.head < 64 ? dq.tail - dq.head : 64;
     if (lane < n) {
@@ -944,7 +945,7 @@ __device__ __forceinline__ void dq_run(DirectQ& dq, float (&acc)[kSlots], bool f
 }
 
 // One element of a trial pass: f(W) and polynomial terms in place; per-candidate elements
-// (|q| > 2^-8) go to the wave's queue.  valid = false: no contribution (still pushes).
+// (|q| > kPolyQ) go to the wave's queue.  valid = false: no contribution (still pushes).
 //
 // Per-candidate form.  With w = |z| (sigmoid) and sg = sign z,
 // sigma(z + d) - sigma(z) = sg [sigma(w + e) - sigma(w)], e = sg d, and with E = exp(-w),
@@ -967,32 +968,46 @@ __device__ __forceinline__ void trial_point(bool valid, float z, float tg, float
     E = __expf(-w);
     const float r = __builtin_amdgcn_rcpf(1.f + E);
     const float sc = E * r;
-    float d0, c1, c2, c3;
+    // Taylor coefficients c_n = phi^(n)(z) / n!, n = 1..5, from phi and phi' (no cancellation)
+    float d0, c1, c2, c3, c4, c5;
     if (TANH) {
       const float mz = 2.f * sc;                    // 1 - |tanh z|
       const float u = copysignf(1.f - mz, z);
-      c1 = mz * (2.f - mz);                         // 1 - u^2
-      c2 = -u * c1;
-      c3 = c1 * (u * u - (1.f / 3.f));
+      const float v = mz * (2.f - mz);              // 1 - u^2
+      const float u2 = u * u;
+      c1 = v;
+      c2 = -u * v;
+      c3 = v * (u2 - (1.f / 3.f));
+      c4 = u * v * (2.f - 3.f * u2) * (1.f / 3.f);
+      c5 = v * (2.f - 15.f * u2 * v) * (1.f / 15.f);
       d0 = copysignf(-expm1_acc(-w) * r, z) - tg;  // tanh z = sg (1 - E) / (1 + E)
     } else {
       const float s = z >= 0.f ? r : sc, s_c = z >= 0.f ? sc : r;   // = sig_pair(z)
-      const float p = s * s_c;
+      const float p = s * s_c, h = s_c - s;        // sigma', 1 - 2 sigma
       c1 = p;
-      c2 = 0.5f * p * (s_c - s);
+      c2 = 0.5f * p * h;
       c3 = p * (1.f - 6.f * p) * (1.f / 6.f);
+      c4 = p * h * (1.f - 12.f * p) * (1.f / 24.f);
+      c5 = p * (1.f - 30.f * p + 120.f * p * p) * (1.f / 120.f);
       d0 = s - tg;
     }
     acc[kSlotFw] += d0 * d0;
-    if (fabsf(qv) <= 0x1p-8f) {
+    if (fabsf(qv) <= kPolyQ) {
       if (pass == 0) {
-        const float a1 = c1 * qv, a2 = c2 * qv * qv, a3 = c3 * qv * qv * qv, t = 2.f * d0;
+        // D(s) = sum_n a_n s^n, a_n = c_n q^n; increment D (2 d0 + D) = sum_j P_j s^j, j = 1..10
+        const float q2 = qv * qv;
+        const float a1 = c1 * qv, a2 = c2 * q2, a3 = c3 * q2 * qv, a4 = c4 * q2 * q2, a5 = c5 * q2 * q2 * qv;
+        const float t = 2.f * d0;
         acc[kSlotPoly + 0] += t * a1;
-        acc[kSlotPoly + 1] += t * a2 + a1 * a1;
-        acc[kSlotPoly + 2] += t * a3 + 2.f * a1 * a2;
-        acc[kSlotPoly + 3] += a2 * a2 + 2.f * a1 * a3;
-        acc[kSlotPoly + 4] += 2.f * a2 * a3;
-        acc[kSlotPoly + 5] += a3 * a3;
+        acc[kSlotPoly + 1] += fmaf(t, a2, a1 * a1);
+        acc[kSlotPoly + 2] += fmaf(t, a3, 2.f * a1 * a2);
+        acc[kSlotPoly + 3] += fmaf(t, a4, fmaf(2.f * a1, a3, a2 * a2));
+        acc[kSlotPoly + 4] += fmaf(t, a5, 2.f * fmaf(a1, a4, a2 * a3));
+        acc[kSlotPoly + 5] += fmaf(2.f * a1, a5, fmaf(2.f * a2, a4, a3 * a3));
+        acc[kSlotPoly + 6] += 2.f * fmaf(a2, a5, a3 * a4);
+        acc[kSlotPoly + 7] += fmaf(2.f * a3, a5, a4 * a4);
+        acc[kSlotPoly + 8] += 2.f * a4 * a5;
+        acc[kSlotPoly + 9] += a5 * a5;
       }
     } else {
       direct = true;
@@ -1005,6 +1020,89 @@ __device__ __forceinline__ void trial_point(bool valid, float z, float tg, float
     }
   }
   dq_push(dq, direct, cr, e, E, w, d2);
+}
+
+// Two elements of a trial pass at once (the fast path's float4 halves), in packed f32
+// (v_pk_fma_f32 / v_pk_mul_f32): same arithmetic as trial_point, branch-free.  Elements past
+// the polynomial bound contribute q = 0 to the polynomial sums and go to the wave's queue.
+// acc2 holds the f(W) sum (slot 0) and the kPolyN polynomial sums (slots 1..kPolyN) per lane
+// pair; they are folded into acc at the end of the pass.
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+constexpr int kPair = kPolyN + 1;
+
+template <bool TANH>
+__device__ __forceinline__ void trial_pair(bool ok, f32x2 z, f32x2 tg, f32x2 qv, int pass, float (&acc)[kSlots],
+                                           f32x2 (&acc2)[kPair], DirectQ& dq, bool ok_y = true) {
+  const f32x2 az = f32x2{fabsf(z.x), fabsf(z.y)};
+  const f32x2 w = TANH ? 2.f * az : az;
+  const f32x2 E = f32x2{__expf(-w.x), __expf(-w.y)};
+  const f32x2 r = f32x2{__builtin_amdgcn_rcpf(1.f + E.x), __builtin_amdgcn_rcpf(1.f + E.y)};
+  const f32x2 sc = E * r;
+  f32x2 d0, c1, c2, c3, c4, c5;
+  if (TANH) {
+    const f32x2 mz = 2.f * sc;                    // 1 - |tanh z|
+    const f32x2 um = 1.f - mz;
+    const f32x2 u = f32x2{copysignf(um.x, z.x), copysignf(um.y, z.y)};
+    const f32x2 v = mz * (2.f - mz);              // 1 - u^2
+    const f32x2 u2 = u * u;
+    c1 = v;
+    c2 = -u * v;
+    c3 = v * (u2 - (1.f / 3.f));
+    c4 = u * v * (2.f - 3.f * u2) * (1.f / 3.f);
+    c5 = v * (2.f - 15.f * u2 * v) * (1.f / 15.f);
+    // |tanh z| = -expm1(-w) r: degree-8 Taylor of expm1 on |w| < 1/2, else exp - 1
+    const f32x2 xm = -w;
+    f32x2 pe = 1.f / 40320.f;
+    pe = pe * xm + 1.f / 5040.f; pe = pe * xm + 1.f / 720.f; pe = pe * xm + 1.f / 120.f;
+    pe = pe * xm + 1.f / 24.f; pe = pe * xm + 1.f / 6.f; pe = pe * xm + 0.5f; pe = pe * xm + 1.f;
+    pe = pe * xm;
+    const f32x2 em = f32x2{w.x < 0.5f ? pe.x : E.x - 1.f, w.y < 0.5f ? pe.y : E.y - 1.f};
+    const f32x2 th = -em * r;
+    d0 = f32x2{copysignf(th.x, z.x), copysignf(th.y, z.y)} - tg;
+  } else {
+    const f32x2 sg = f32x2{z.x >= 0.f ? r.x : sc.x, z.y >= 0.f ? r.y : sc.y};   // sigma(z)
+    const f32x2 sgc = f32x2{z.x >= 0.f ? sc.x : r.x, z.y >= 0.f ? sc.y : r.y};  // 1 - sigma(z)
+    const f32x2 p = sg * sgc, h = sgc - sg;
+    c1 = p;
+    c2 = 0.5f * p * h;
+    c3 = p * (1.f - 6.f * p) * (1.f / 6.f);
+    c4 = p * h * (1.f - 12.f * p) * (1.f / 24.f);
+    c5 = p * (1.f - 30.f * p + 120.f * p * p) * (1.f / 120.f);
+    d0 = sg - tg;
+  }
+  const f32x2 okm = f32x2{ok ? 1.f : 0.f, ok && ok_y ? 1.f : 0.f};
+  d0 = d0 * okm;
+  acc2[0] += d0 * d0;
+  const bool px = fabsf(qv.x) <= kPolyQ, py = fabsf(qv.y) <= kPolyQ;
+  if (pass == 0) {
+    const f32x2 qp = f32x2{px ? qv.x : 0.f, py ? qv.y : 0.f};
+    const f32x2 q2 = qp * qp;
+    const f32x2 a1 = c1 * qp, a2 = c2 * q2, a3 = c3 * q2 * qp, a4 = c4 * q2 * q2, a5 = c5 * q2 * q2 * qp;
+    const f32x2 t = 2.f * d0;
+    acc2[1] += t * a1;
+    acc2[2] += t * a2 + a1 * a1;
+    acc2[3] += t * a3 + 2.f * a1 * a2;
+    acc2[4] += t * a4 + 2.f * a1 * a3 + a2 * a2;
+    acc2[5] += t * a5 + 2.f * (a1 * a4 + a2 * a3);
+    acc2[6] += 2.f * (a1 * a5 + a2 * a4) + a3 * a3;
+    acc2[7] += 2.f * (a2 * a5 + a3 * a4);
+    acc2[8] += 2.f * a3 * a5 + a4 * a4;
+    acc2[9] += 2.f * a4 * a5;
+    acc2[10] += a5 * a5;
+  }
+  // per-candidate elements: sigma(w + e) - sigma(w) form (see trial_point)
+  const f32x2 f2sg = f32x2{(TANH ? 2.f : 1.f) * (z.x >= 0.f ? 1.f : -1.f), (TANH ? 2.f : 1.f) * (z.y >= 0.f ? 1.f : -1.f)};
+  const float s0 = ldexpf(1.f, -(pass * kTrialJ + kTrialJ - 1));   // smallest candidate
+  const bool dx = ok && !px, dy = ok && ok_y && !py;
+  acc[kSlotNne] += (dx ? 1.f : 0.f) + (dy ? 1.f : 0.f);
+  dq_push(dq, dx, -f2sg.x * r.x, f2sg.x * qv.x * s0, E.x, w.x, 2.f * d0.x);
+  dq_push(dq, dy, -f2sg.y * r.y, f2sg.y * qv.y * s0, E.y, w.y, 2.f * d0.y);
+}
+
+__device__ __forceinline__ void trial_pair_fold(float (&acc)[kSlots], const f32x2 (&acc2)[kPair]) {
+  acc[kSlotFw] += acc2[0].x + acc2[0].y;
+#pragma unroll
+  for (int n = 0; n < kPolyN; ++n) acc[kSlotPoly + n] += acc2[n + 1].x + acc2[n + 1].y;
 }
 
 __device__ __forceinline__ void trial_block_store(float (&acc)[kSlots], double* part, int q, int blk, int nblk) {
@@ -1138,7 +1236,7 @@ __device__ __forceinline__ float4 xw_row(const float (&xr)[DP], const float4* __
 // (Wlds = G_x of this gate in LDS); side 1 reads Q.
 constexpr int kRPI = 2;
 
-template <bool TANH, int SIDE, int DP, bool XV>
+template <bool TANH, int SIDE, int DP, bool XV, bool UR>
 __device__ __forceinline__ void trial_fast_body(const Geom& g, int q, int pass, const float* __restrict__ zc,
                                                 const float* __restrict__ tgt, const float* __restrict__ Q,
                                                 const float* __restrict__ x, const float* Wlds, int blk, int nblk,
@@ -1151,58 +1249,71 @@ __device__ __forceinline__ void trial_fast_body(const Geom& g, int q, int pass, 
   RowCols rc(g.H);
   const bool lane_ok = rc.rr < rc.rpb;     // idle lanes stay in the (wave-uniform) loop
   const int j = 4 * rc.c4, H4 = g.H / 4;   // fast path: H/4 <= 256, one float4 column per thread
-  constexpr int kRPI = SIDE == 0 ? 1 : 2;   // side 0 keeps its x rows live: one row per pass
   const int64_t stride = (int64_t)nblk * rc.rpb;
-  for (int64_t base = (int64_t)blk * rc.rpb; base < BT; base += kRPI * stride) {
-    const int64_t row0 = base + rc.rr;
-    float4 z4[kRPI], t4[kRPI], q4[kRPI];
-    float xr[kRPI][DP];
-    bool ok[kRPI];
+  // one row per thread per iteration, the next row's operands loaded while this one is
+  // evaluated (branch-free: rows past the end are loaded clamped and masked by ok)
+  struct In { float4 z, t, q; float xr[DP]; };
+  auto load = [&](int64_t row, In& v) {
+    const int64_t rr = row < BT ? row : BT - 1;
+    v.z = ld_nt(zq + rr * g.H + j);
+    v.t = ld_nt(tq + rr * g.H + j);
+    // UR: one row per wave (H/4 a multiple of 64), so the x row is wave-uniform: scalar loads
+    // into SGPRs instead of 16 VGPRs per row in flight
+    if (SIDE == 0) load_xrow<DP, XV>(x, UR ? (int64_t)__builtin_amdgcn_readfirstlane((int)rr) : rr, g.D, v.xr);
+    else v.q = ld_nt(Qq + rr * g.H + j);
+  };
+#ifndef TF_ABL
+#define TF_ABL 0   // trial ablations for tools/kbench (bitmask, 0 = full kernel)
+#endif
+  int64_t base = (int64_t)blk * rc.rpb;
+  f32x2 acc2[kPair];
 #pragma unroll
-    for (int r = 0; r < kRPI; ++r) {
-      const int64_t row = row0 + r * stride;
-      ok[r] = lane_ok && row < BT;
-      z4[r] = t4[r] = q4[r] = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (SIDE == 0) {
+  for (int k = 0; k < kPair; ++k) acc2[k] = f32x2{0.f, 0.f};
+  In cur, nxt;
+  load(base + rc.rr, cur);
+  for (; base < BT; base += stride) {
+    const bool ok = lane_ok && base + rc.rr < BT;
+    load(base + stride + rc.rr, nxt);
+    float4 q4 = cur.q;
+    if (SIDE == 0) {
+      q4 = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (!(TF_ABL & 1)) {   // q = x_row . G_x; G_x reads in groups of 4 issued back to back
+        const float4* wrow = wl4 + rc.c4;
 #pragma unroll
-        for (int d = 0; d < DP; ++d) xr[r][d] = 0.f;
-      }
-      if (ok[r]) {
-        z4[r] = ld_nt(zq + row * g.H + j);
-        t4[r] = ld_nt(tq + row * g.H + j);
-        if (SIDE == 0) load_xrow<DP, XV>(x, row, g.D, xr[r]);
-        else q4[r] = ld_nt(Qq + row * g.H + j);
-      }
-    }
-    if (SIDE == 0) {   // q = x_row . G_x for both rows, one LDS read of G_x per d
+        for (int d0 = 0; d0 < DP; d0 += 4) {
+          float4 wv[4];
 #pragma unroll
-      for (int d = 0; d < DP; ++d) {
-        const float4 wv = wl4[d * H4 + rc.c4];
+          for (int i = 0; i < 4; ++i) wv[i] = wrow[(d0 + i) * H4];
 #pragma unroll
-        for (int r = 0; r < kRPI; ++r) {
-          q4[r].x = fmaf(xr[r][d], wv.x, q4[r].x); q4[r].y = fmaf(xr[r][d], wv.y, q4[r].y);
-          q4[r].z = fmaf(xr[r][d], wv.z, q4[r].z); q4[r].w = fmaf(xr[r][d], wv.w, q4[r].w);
+          for (int i = 0; i < 4; ++i) {
+            const float xv = cur.xr[d0 + i];
+            q4.x = fmaf(xv, wv[i].x, q4.x); q4.y = fmaf(xv, wv[i].y, q4.y);
+            q4.z = fmaf(xv, wv[i].z, q4.z); q4.w = fmaf(xv, wv[i].w, q4.w);
+          }
         }
       }
     }
-#pragma unroll
-    for (int r = 0; r < kRPI; ++r) {
-#pragma unroll 1
-      for (int u = 0; u < 4; ++u) {
-        const float zu = u == 0 ? z4[r].x : (u == 1 ? z4[r].y : (u == 2 ? z4[r].z : z4[r].w));
-        const float tu = u == 0 ? t4[r].x : (u == 1 ? t4[r].y : (u == 2 ? t4[r].z : t4[r].w));
-        const float qu = u == 0 ? q4[r].x : (u == 1 ? q4[r].y : (u == 2 ? q4[r].z : q4[r].w));
-        trial_point<TANH>(ok[r], zu, tu, qu, pass, acc, dq);
-        dq_run(dq, acc, false);
-      }
+    if (TF_ABL & 2) {
+      acc[0] += cur.z.x * cur.t.x + q4.x + cur.z.y * cur.t.y + q4.y;
+      acc[1] += cur.z.z * cur.t.z + q4.z + cur.z.w * cur.t.w + q4.w;
+    } else {
+      trial_pair<TANH>(ok, f32x2{cur.z.x, cur.z.y}, f32x2{cur.t.x, cur.t.y}, f32x2{q4.x, q4.y}, pass, acc, acc2, dq);
+      if (!(TF_ABL & 4)) dq_run(dq, acc, false);
+      trial_pair<TANH>(ok, f32x2{cur.z.z, cur.z.w}, f32x2{cur.t.z, cur.t.w}, f32x2{q4.z, q4.w}, pass, acc, acc2, dq);
+      if (!(TF_ABL & 4)) dq_run(dq, acc, false);
     }
+    cur = nxt;
   }
+  trial_pair_fold(acc, acc2);
   dq_run(dq, acc, true);
 }
 
 // Wsrc: side 0 -> G_x [4][D][H]; side 1 -> unused (Q holds the h-side direction)
-template <int SIDE, int DP, bool XV>
-__global__ __launch_bounds__(kThreads) void k_trial_fast(Geom g, int pass, const float* zc, const float* tgt,
+#ifndef TF_MINB
+#define TF_MINB 3   // workgroups per CU the register allocation must allow (occupancy for the streams)
+#endif
+template <int SIDE, int DP, bool XV, bool UR>
+__global__ __launch_bounds__(kThreads, TF_MINB) void k_trial_fast(Geom g, int pass, const float* zc, const float* tgt,
                                                            const float* Q, const float* x, const float* Wsrc,
                                                            const int* found, double* part, int nblk) {
   extern __shared__ float wlds[];  // [DP][H] (side 0 only)
@@ -1214,9 +1325,90 @@ __global__ __launch_bounds__(kThreads) void k_trial_fast(Geom g, int pass, const
   for (int k = 0; k < kSlots; ++k) acc[k] = 0.f;
   __shared__ float dqbuf[kThreads / 64][5 * kDQ];
   DirectQ dq{dqbuf[threadIdx.x >> 6], 0, 0};
-  if (q == 2) trial_fast_body<true, SIDE, DP, XV>(g, q, pass, zc, tgt, Q, x, wlds, blk, nblk, acc, dq);
-  else trial_fast_body<false, SIDE, DP, XV>(g, q, pass, zc, tgt, Q, x, wlds, blk, nblk, acc, dq);
+  if (q == 2) trial_fast_body<true, SIDE, DP, XV, UR>(g, q, pass, zc, tgt, Q, x, wlds, blk, nblk, acc, dq);
+  else trial_fast_body<false, SIDE, DP, XV, UR>(g, q, pass, zc, tgt, Q, x, wlds, blk, nblk, acc, dq);
   trial_block_store(acc, part, q, blk, nblk);
+}
+
+// Trial pass for H % 256 == 0 (the C3/C4/C5 shapes): a workgroup owns 256 columns j, one per
+// thread, and walks row pairs.  The row pair is the same for the whole workgroup, so the x rows
+// are wave-uniform (scalar loads, SGPR operands) and the thread's column of G_x stays in 16
+// VGPRs for the whole pass: q = x_row . G_x costs 16 FMAs and no LDS.  The two rows are the two
+// halves of trial_pair's packed arithmetic; the next pair's operands are loaded while this one
+// is evaluated.  Side 1 reads q from Q instead.
+template <bool TANH, int SIDE, int DP, bool XV>
+__device__ __forceinline__ void trial_rows_body(const Geom& g, int q, int pass, const float* __restrict__ zc,
+                                                const float* __restrict__ tgt, const float* __restrict__ Q,
+                                                const float* __restrict__ x, const float* __restrict__ Gx, int blk,
+                                                int nblk, float (&acc)[kSlots], DirectQ& dq) {
+  const int64_t BT = g.BT(), n = BT * g.H;
+  const int j = blockIdx.z * 256 + threadIdx.x;
+  const float* __restrict__ zq = zc + (int64_t)q * n + j;
+  const float* __restrict__ tq = tgt + (int64_t)q * n + j;
+  const float* __restrict__ Qq = Q ? Q + (int64_t)q * n + j : nullptr;
+  float gw[DP];
+#pragma unroll
+  for (int d = 0; d < DP; ++d) gw[d] = (SIDE == 0 && d < g.D) ? Gx[((int64_t)q * g.D + d) * g.H + j] : 0.f;
+  struct In { f32x2 z, t, q; float xa[DP], xb[DP]; };
+  auto load = [&](int64_t ra, In& v) {   // rows ra, ra + 1 (clamped)
+    const int64_t r0 = __builtin_amdgcn_readfirstlane((int)(ra < BT ? ra : BT - 1));
+    const int64_t r1 = __builtin_amdgcn_readfirstlane((int)(ra + 1 < BT ? ra + 1 : BT - 1));
+    v.z = f32x2{__builtin_nontemporal_load(zq + r0 * g.H), __builtin_nontemporal_load(zq + r1 * g.H)};
+    v.t = f32x2{__builtin_nontemporal_load(tq + r0 * g.H), __builtin_nontemporal_load(tq + r1 * g.H)};
+    if (SIDE == 0) {
+      load_xrow<DP, XV>(x, r0, g.D, v.xa);
+      load_xrow<DP, XV>(x, r1, g.D, v.xb);
+    } else {
+      v.q = f32x2{__builtin_nontemporal_load(Qq + r0 * g.H), __builtin_nontemporal_load(Qq + r1 * g.H)};
+    }
+  };
+  f32x2 acc2[kPair];
+#pragma unroll
+  for (int k = 0; k < kPair; ++k) acc2[k] = f32x2{0.f, 0.f};
+  const int64_t stride = 2 * (int64_t)nblk;
+  int64_t base = 2 * (int64_t)blk;
+  In cur, nxt;
+  load(base, cur);
+  for (; base < BT; base += stride) {
+    load(base + stride, nxt);
+    f32x2 qv = cur.q;
+    if (SIDE == 0) {
+      float qa = 0.f, qb = 0.f;   // scalar FMAs with the (uniform, SGPR) x values as operands
+#pragma unroll
+      for (int d = 0; d < DP; ++d) {
+        qa = fmaf(cur.xa[d], gw[d], qa);
+        qb = fmaf(cur.xb[d], gw[d], qb);
+      }
+      qv = f32x2{qa, qb};
+    }
+    // row base + 1 may be past the end (odd BT): masked through its q and d0 (ok covers the pair)
+    const bool ok1 = base + 1 < BT;
+    trial_pair<TANH>(true, cur.z, ok1 ? cur.t : f32x2{cur.t.x, 0.f},
+                     ok1 ? qv : f32x2{qv.x, 0.f}, pass, acc, acc2, dq, ok1);
+    dq_run(dq, acc, false);
+    cur = nxt;
+  }
+  trial_pair_fold(acc, acc2);
+  dq_run(dq, acc, true);
+}
+
+template <int SIDE, int DP, bool XV>
+__global__ __launch_bounds__(kThreads) void k_trial_rows(Geom g, int pass, const float* __restrict__ zc,
+                                                         const float* __restrict__ tgt, const float* __restrict__ Q,
+                                                         const float* __restrict__ x, const float* __restrict__ Gx,
+                                                         const int* __restrict__ found, double* __restrict__ part,
+                                                         int nblk) {
+  const int q = blockIdx.y, blk = blockIdx.x;
+  if (found[q]) return;
+  float acc[kSlots];
+#pragma unroll
+  for (int k = 0; k < kSlots; ++k) acc[k] = 0.f;
+  __shared__ float dqbuf[kThreads / 64][5 * kDQ];
+  DirectQ dq{dqbuf[threadIdx.x >> 6], 0, 0};
+  if (q == 2) trial_rows_body<true, SIDE, DP, XV>(g, q, pass, zc, tgt, Q, x, Gx, blk, nblk, acc, dq);
+  else trial_rows_body<false, SIDE, DP, XV>(g, q, pass, zc, tgt, Q, x, Gx, blk, nblk, acc, dq);
+  // the column blocks of one (blk, q) add into the same part slot row: blk index widened by z
+  trial_block_store(acc, part, q, blockIdx.z * nblk + blk, nblk * gridDim.z);
 }
 
 // After the x stage: zc += X dWx, so the h stage sees z = X Wx_new + Hprev Wh
@@ -1890,16 +2082,36 @@ void launch_apply_dwx(const Geom& g, const float* x, const float* dW, float* zc,
   });
 }
 
+bool trial_rows_ok(const Geom& g) { return g.H % 256 == 0; }
+
 void launch_trial_fast(const Geom& g, int side, int pass, const float* zc, const float* tgt, const float* Q,
                        const float* x, const float* Wsrc, const int* found, double* part, int nblk, hipStream_t s) {
   dim3 grid(nblk, 4);
-  if (side == 1) {  // no x . W product on this side: one instantiation
-    k_trial_fast<1, 4, false><<<grid, kThreads, 0, s>>>(g, pass, zc, tgt, Q, x, Wsrc, found, part, nblk);
+  if (side == 1 && trial_rows_ok(g)) {
+    dim3 gr(nblk, 4, g.H / 256);
+    k_trial_rows<1, 4, false><<<gr, kThreads, 0, s>>>(g, pass, zc, tgt, Q, x, Wsrc, found, part, nblk);
     return;
   }
+  if (side == 1) {  // no x . W product on this side: one instantiation
+    k_trial_fast<1, 4, false, false><<<grid, kThreads, 0, s>>>(g, pass, zc, tgt, Q, x, Wsrc, found, part, nblk);
+    return;
+  }
+  if (trial_rows_ok(g)) {
+    dim3 gr(nblk, 4, g.H / 256);
+    with_dp(g, [&](auto dp, auto xv) {
+      k_trial_rows<0, decltype(dp)::value, decltype(xv)::value>
+          <<<gr, kThreads, 0, s>>>(g, pass, zc, tgt, Q, x, Wsrc, found, part, nblk);
+    });
+    return;
+  }
+  const bool ur = (g.H / 4) % 64 == 0;   // one row per wave
   with_dp(g, [&](auto dp, auto xv) {
-    k_trial_fast<0, decltype(dp)::value, decltype(xv)::value>
-        <<<grid, kThreads, fast_lds(g), s>>>(g, pass, zc, tgt, Q, x, Wsrc, found, part, nblk);
+    if (ur)
+      k_trial_fast<0, decltype(dp)::value, decltype(xv)::value, true>
+          <<<grid, kThreads, fast_lds(g), s>>>(g, pass, zc, tgt, Q, x, Wsrc, found, part, nblk);
+    else
+      k_trial_fast<0, decltype(dp)::value, decltype(xv)::value, false>
+          <<<grid, kThreads, fast_lds(g), s>>>(g, pass, zc, tgt, Q, x, Wsrc, found, part, nblk);
   });
 }
 

@@ -7,8 +7,9 @@
 namespace admm {
 
 constexpr int kTrialJ = 16;      // line-search candidates evaluated per trial pass
-// per-gate sums of a trial pass: [J candidates][6 polynomial coefficients][sum d0^2][#per-candidate elements]
-constexpr int kPolyN = 6;
+// per-gate sums of a trial pass: [J candidates][10 polynomial coefficients][sum d0^2][#per-candidate elements]
+constexpr int kPolyN = 10;
+constexpr float kPolyQ = 0x1p-5f;   // |q| bound of the polynomial (5-term Taylor) regime
 constexpr int kTrialSlots = kTrialJ + kPolyN + 2;
 constexpr int kMaxK = 96;        // exponents decided from the polynomial alone go up to this
 constexpr int kMaxPasses = 4;    // => exponents k in [0, 64)
@@ -151,6 +152,9 @@ void launch_resid_gx(const Geom& g, const Hyper& hp, const float* x, const Plane
 void launch_trial_fast(const Geom& g, int side, int pass, const float* zc, const float* tgt, const float* Q,
                        const float* x, const float* Wsrc, const int* found, double* part, int nblk, hipStream_t s);
 int stream_blocks(const Geom& g);   // grid (per gate) of the fast streaming passes
+// H % 256 == 0: the fast trial passes run as row-pair workgroups over H/256 column blocks, and
+// write stream_blocks(g) * H/256 partials per slot (the reduce's nblk)
+bool trial_rows_ok(const Geom& g);
 // after the x stage (fast path): zc += X dWx
 void launch_apply_dwx(const Geom& g, const float* x, const float* dW, float* zc, hipStream_t s);
 // h stage A^T R with R computed on the fly from zc (already updated) and tgt (side 1, fast path)

@@ -190,7 +190,9 @@ def test_teacher_forced_steps(name, mods, dev):
 
 
 @pytest.mark.parametrize('shape,variant', [((256, 6, 4, 32), 'admm'), ((300, 5, 16, 48), 'admm'),
-                                           ((200, 8, 1, 12), 'no_dual_y'), ((512, 4, 8, 64), 'admm')])
+                                           ((200, 8, 1, 12), 'no_dual_y'), ((512, 4, 8, 64), 'admm'),
+                                           # H % 256 == 0: split-bf16 h-stage GEMMs, row-pair trials
+                                           ((256, 3, 16, 256), 'admm'), ((160, 2, 3, 512), 'no_dual_y')])
 def test_line_search_matches_fp64_oracle(shape, variant, mods, dev):
     """From a perturbed state (the consistent initial state plus 1e-2 noise on gates and
     duals: weight gradients well above fp32 rounding), one GPU step vs one fp64 oracle
@@ -260,6 +262,33 @@ def test_trial_increments_vs_fp64(tanh_gate, dev):
             ref = inc.sum()
             scale = np.abs(inc).sum()
             assert abs(out[k] - ref) <= 2e-5 * scale + 1e-30, (kk, out[k], ref, scale)
+
+
+@pytest.mark.parametrize('tanh_gate', [0, 1])
+def test_trial_polynomial_band_vs_fp64(tanh_gate, dev):
+    """Elements at the top of the polynomial regime (|q| in [2^-9, 2^-5]: 5-term Taylor in s,
+    admm_kernels.hpp kPolyQ), every exponent of the first two windows, vs numpy fp64."""
+    from admm_amd import _native as N
+    lib = N.load()
+    rng = np.random.default_rng(6)
+    n = 100_000
+    z = rng.normal(0, 2.5, n).astype(np.float32)
+    phi = np.tanh if tanh_gate else (lambda v: 1 / (1 + np.exp(-v)))
+    tgt = (phi(z.astype(np.float64)) + rng.normal(0, 1e-3, n)).astype(np.float32)
+    q = (rng.choice([-1.0, 1.0], n) * 2.0 ** rng.uniform(-9, -5, n)).astype(np.float32)
+    zt, tt, qt = (torch.from_numpy(a).to(dev) for a in (z, tgt, q))
+    z64, t64, q64 = z.astype(np.float64), tgt.astype(np.float64), q.astype(np.float64)
+    d0 = phi(z64) - t64
+    for kbase in (0, 16):
+        out = (ctypes.c_double * 16)()
+        N.check(lib.admm_debug_trial(N.ptr(zt), N.ptr(tt), N.ptr(qt), n, tanh_gate, kbase, out,
+                                     N.stream_handle(dev)), 'admm_debug_trial')
+        for k in range(16):
+            kk = kbase + k
+            d1 = phi(z64 + q64 * 2.0 ** -kk) - t64
+            inc = (d1 - d0) * (d1 + d0)
+            ref, scale = inc.sum(), np.abs(inc).sum()
+            assert abs(out[k] - ref) <= 2e-6 * scale + 1e-30, (kk, out[k], ref, scale)
 
 
 def test_forward_matches_oracle(dev):

@@ -6,6 +6,7 @@
 #include <functional>
 #include <random>
 #include <vector>
+#include <string>
 #include <cmath>
 #include <algorithm>
 #include "../admm-lstm_amd/admm_amd/csrc/admm_kernels.hpp"
@@ -103,7 +104,8 @@ int main(int argc, char** argv) {
     printf("qgemm3 vs qgemm: max |diff| %.3e (max |Q| %.3e, rel %.2e)\n", md, mx, md / mx);
   }
   };
-  if (argc > 2) { run_s3(); return 0; }
+  const std::string mode = argc > 2 ? argv[2] : "";
+  if (mode == "s3") { run_s3(); return 0; }
   timeit("apply_dwx", 2 * f4 * 4 * n + f4 * BT * g.D, 0, [&] { launch_apply_dwx(g, x, dW, zc, s); });
   timeit("trial_fast side0", f4 * 2 * 4 * n, 0, [&] { launch_trial_fast(g, 0, 0, zc, tgt, nullptr, x, G, found, part, nb, s); });
   timeit("trial_fast side1", f4 * 3 * 4 * n, 0, [&] { launch_trial_fast(g, 1, 0, zc, tgt, Q, x, dW, found, part, nb, s); });
@@ -116,6 +118,7 @@ int main(int argc, char** argv) {
     timeit("trial_fast side1 |q|<.01", f4 * 3 * 4 * n, 0, [&] { launch_trial_fast(g, 1, 0, zc, tgt, Qm, x, dW, found, part, nb, s); });
     (void)hipFree(Qb); (void)hipFree(Qm); (void)hipFree(G0);
   }
+  if (mode == "tr") return 0;
   timeit("trial generic", f4 * 3 * 4 * n, 0, [&] { launch_trial(g, 0, zc, tgt, Q, found, part, trial_blocks(g), s); });
   timeit("resid_gx", f4 * 4 * 4 * n, 0, [&] { launch_resid_gx(g, hp, x, S, L, zc, tgt, slab, resid_gx_blocks(g), s); });
   const int ns = atr_splits(g, 1);

@@ -1,0 +1,2 @@
+set -e
+for v in "$@"; do echo "== kbench$v"; timeout -k 5 60 ./tools/kbench$v 8192 tr; done

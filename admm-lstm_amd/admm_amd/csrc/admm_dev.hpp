@@ -189,6 +189,7 @@ __device__ __forceinline__ int xcd_swizzle(int bid, int nb) {
 // Raw buffer access (gfx9 descriptor word 3; aux 2 = nt).  Out-of-range offsets (>= the
 // descriptor's byte count) load 0 and drop stores.
 constexpr int kBufWord3 = 0x00020000;
+constexpr int kAuxL2 = 1 | 16;   // buffer cache policy sc0 | sc1 (gfx940+): coherent at device scope, misses the L1
 template <int AUX = 2>
 __device__ __forceinline__ float buf_ld(__amdgpu_buffer_rsrc_t r, uint32_t off) {
   return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, (int)off, 0, AUX));
@@ -201,6 +202,12 @@ template <int AUX = 2>
 __device__ __forceinline__ void buf_st4(__amdgpu_buffer_rsrc_t r, uint32_t off, f32x4 v) {
   __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned int, v), r,
                                          (int)off, 0, AUX);
+}
+// store at voffset + soffset (soffset wave-uniform: one descriptor serves several planes)
+template <int AUX = 2>
+__device__ __forceinline__ void buf_st4s(__amdgpu_buffer_rsrc_t r, uint32_t off, uint32_t soff, f32x4 v) {
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned int, v), r,
+                                         (int)off, (int)soff, AUX);
 }
 template <int AUX = 2>
 __device__ __forceinline__ void buf_st(__amdgpu_buffer_rsrc_t r, uint32_t off, float v) {

@@ -66,6 +66,12 @@ struct AdmmCtx {
   AdmmBuffers buf{};
   bool bound = false;
   bool z_valid = false;
+  bool force_generic = false;  // weight stages on the generic kernels (ADMM_GENERIC=1; tests)
+  bool tgt_valid = false;  // tgt holds lam/rho + S of the current state (left by the persistent sweep)
+  // let the persistent sweep write tgt for the next x stage (ADMM_TGT_SWEEP=1).  Off: with it on,
+  // C2 trajectories turn non-finite at a random step (x stage of gate g) although z and tgt
+  // are finite and tgt equals lam/rho + S when checked on device; not yet understood
+  bool tgt_sweep = false;
   int steps = 0;
   // workspace (all device)
   float *zc = nullptr, *tgt = nullptr, *R = nullptr, *Q = nullptr;  // [4][BT][H]
@@ -177,7 +183,7 @@ int stage_wy(AdmmCtx* c, hipStream_t s) {
 int stage_weights(AdmmCtx* c, int side, hipStream_t s) {
   const Geom& g = c->g;
   const int Kd = side == 0 ? g.D : g.H;
-  const bool fast = fast_path(g);
+  const bool fast = fast_path(g) && !c->force_generic;
   const Planes6 S = planes(c->buf.gates), L = planes(c->buf.duals);
   HIP_TRY(hipMemsetAsync(c->found, 0, 4 * sizeof(int), s));
   if (fast && side == 1) {  // z of the h-side searches uses the updated x2q (admm.py:298-300)
@@ -189,7 +195,7 @@ int stage_weights(AdmmCtx* c, int side, hipStream_t s) {
   if (fast && side == 0) {
     ns = c->nblk_rx;
     ProfScope ps(c, ADMM_PROF_RESID, s);
-    launch_resid_gx(g, c->hp, c->buf.x, S, L, c->zc, c->tgt, c->gslab, ns, s);
+    launch_resid_gx(g, c->hp, c->buf.x, S, L, c->zc, c->tgt, c->gslab, ns, c->tgt_valid && c->z_valid, s);
   } else if (fast && c->split3) {
     ns = atr3_splits(g);
     ProfScope ps(c, ADMM_PROF_ATR_H, s);
@@ -272,6 +278,7 @@ int stage_sweep(AdmmCtx* c, hipStream_t s) {
     ProfScope ps(c, ADMM_PROF_SWEEP, s);
     sa.r0 = 0;
     sa.r1 = g.B;
+    sa.tgt = fast_path(g) && c->tgt_sweep ? c->tgt : nullptr;   // the fast x stage reads it next step
     launch_sweep_wt(g, w, c->swt, s);
     launch_sweep_rows(g, c->swt, c->hp, sa, s);
   } else {
@@ -359,6 +366,8 @@ int admm_create(const AdmmDims* dims, const AdmmParams* params, int device, Admm
     c->sweep_split = std::max(1, std::min(kMaxSweepStreams, std::atoi(e)));
   c->sweep_rows = sweep_rows_ok(g);
   if (const char* e = std::getenv("ADMM_SWEEP_ROWS")) c->sweep_rows = c->sweep_rows && std::atoi(e) != 0;
+  if (const char* e = std::getenv("ADMM_TGT_SWEEP")) c->tgt_sweep = std::atoi(e) != 0;
+  if (const char* e = std::getenv("ADMM_GENERIC")) c->force_generic = std::atoi(e) != 0;
   c->split3 = fast_path(g) && split3_ok(g);
   if (const char* e = std::getenv("ADMM_SPLIT3")) c->split3 = c->split3 && std::atoi(e) != 0;
   Hyper& h = c->hp;
@@ -382,7 +391,7 @@ int admm_create(const AdmmDims* dims, const AdmmParams* params, int device, Admm
   if (c->split3) slab = std::max(slab, (size_t)atr3_splits(g) * 4 * g.H * g.H);
   c->wy_nsplit = wy_splits(g);
   c->ht_nblk = ht_blocks(g);
-  if ((rc = dalloc(&c->zc, 4 * plane)) || (rc = dalloc(&c->tgt, 4 * plane)) || (rc = dalloc(&c->R, fast_path(g) ? 1 : 4 * plane)) ||
+  if ((rc = dalloc(&c->zc, 4 * plane)) || (rc = dalloc(&c->tgt, 4 * plane)) || (rc = dalloc(&c->R, fast_path(g) && !c->force_generic ? 1 : 4 * plane)) ||
       (rc = dalloc(&c->Q, 4 * plane)) || (rc = dalloc(&c->G, (size_t)4 * Kmax * g.H)) ||
       (rc = dalloc(&c->dW, (size_t)4 * g.D * g.H)) ||
       (rc = dalloc(&c->gslab, slab)) ||
@@ -448,6 +457,7 @@ int admm_bind(AdmmCtx* c, const AdmmBuffers* b) {
   c->buf = *b;
   c->bound = true;
   c->z_valid = false;
+  c->tgt_valid = false;
   return ADMM_OK;
 }
 
@@ -460,6 +470,7 @@ int admm_set_with_dual_y(AdmmCtx* c, int32_t flag) {
 int admm_invalidate_cache(AdmmCtx* c) {
   if (!c) return fail(ADMM_EINVAL, "NULL ctx");
   c->z_valid = false;
+  c->tgt_valid = false;
   return ADMM_OK;
 }
 
@@ -496,6 +507,7 @@ int admm_init_state(AdmmCtx* c, void* stream) {
   launch_rowdot(g.B, g.H, g.O, c->buf.gates[ADMM_H] + (int64_t)g.T * g.H, rs, c->buf.wy, c->buf.a, s);
   HIP_TRY(hipGetLastError());
   c->z_valid = true;
+  c->tgt_valid = false;   // recomputed from the new state by the first x stage
   return ADMM_OK;
 }
 
@@ -515,6 +527,7 @@ int admm_step(AdmmCtx* c, void* stream) {
   if ((rc = stage_sweep(c, s))) return rc;
   HIP_TRY(hipGetLastError());
   c->z_valid = true;  // the sweep left x_t Wx + h_{t-1} Wh of the final state in the cache
+  c->tgt_valid = c->sweep_rows && fast_path(c->g) && c->tgt_sweep;
   c->steps++;
   return ADMM_OK;
 }
@@ -589,6 +602,19 @@ int admm_get_stats(AdmmCtx* c, AdmmStats* out) {
   out->unresolved = d.unresolved;
   out->nonfinite = d.nonfinite;
   return ADMM_OK;
+}
+
+int admm_debug_workspace(AdmmCtx* c, int32_t which, void* dst, int64_t bytes, void* stream) {
+  if (!c || !dst) return fail(ADMM_EINVAL, "admm_debug_workspace: NULL argument");
+  const int64_t need = (int64_t)4 * c->g.BT() * c->g.H * (int64_t)sizeof(float);
+  if (bytes < need) return fail(ADMM_EINVAL, "admm_debug_workspace: %lld bytes < %lld", (long long)bytes, (long long)need);
+  const float* src = which == 0 ? c->zc : which == 1 ? c->tgt : nullptr;
+  if (!src) return fail(ADMM_EINVAL, "admm_debug_workspace: unknown array %d", which);
+  HIP_TRY(hipSetDevice(c->device));
+  hipStream_t s = (hipStream_t)stream;
+  HIP_TRY(hipMemcpyAsync(dst, src, need, hipMemcpyDeviceToDevice, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  return which == 0 ? (c->z_valid ? 1 : 0) : (c->tgt_valid && c->z_valid ? 1 : 0);
 }
 
 int admm_debug_trial(const float* z, const float* tgt, const float* q, int64_t n, int32_t tanh_gate, int32_t kbase,

@@ -395,14 +395,19 @@ __global__ __launch_bounds__(SR_THREADS) void k_sweep_rows(Geom g, const bf16x8*
   const int ct = threadIdx.x - 4 * 64;      // 0..255
   const int row = ct >> 3, j4 = (ct & 7) * 4;
   const uint32_t pbytes = (uint32_t)(a.r1 * rs * 4), zbytes = (uint32_t)(a.r1 * T * H * 4);
-  __amdgpu_buffer_rsrc_t rS[6], rL[6], rZ[4];
+  __amdgpu_buffer_rsrc_t rS[6], rL[6];
 #pragma unroll
   for (int p = 0; p < 6; ++p) {
     rS[p] = __builtin_amdgcn_make_buffer_rsrc(a.S.p[p], 0, pbytes, kBufWord3);
     rL[p] = __builtin_amdgcn_make_buffer_rsrc(a.L.p[p], 0, pbytes, kBufWord3);
   }
-#pragma unroll
-  for (int q = 0; q < 4; ++q) rZ[q] = __builtin_amdgcn_make_buffer_rsrc(a.zc + q * BTH, 0, zbytes, kBufWord3);
+  // z cache and lam/rho + S of the updated i, f, g, o (the next step's x-stage targets): one
+  // descriptor per [4][B*T][H] array, the gate plane selected by soffset
+  const uint32_t zpl = (uint32_t)(BTH * 4), zrec = 3 * zpl + zbytes;   // plane stride, records
+  const __amdgpu_buffer_rsrc_t rZ = __builtin_amdgcn_make_buffer_rsrc(a.zc, 0, zrec, kBufWord3);
+  const bool wtgt = a.tgt != nullptr;
+  const __amdgpu_buffer_rsrc_t rT = __builtin_amdgcn_make_buffer_rsrc(wtgt ? a.tgt : a.zc, 0, wtgt ? zrec : 0, kBufWord3);
+  const bool rok = m0 + row < a.r1;
   const uint32_t pofs = (uint32_t)(((m0 + row) * rs + j4) * 4);       // t = 0, tile 0
   const uint32_t zofs = (uint32_t)(((m0 + row) * T * H + j4) * 4);    // t = 1, tile 0
 
@@ -410,7 +415,9 @@ __global__ __launch_bounds__(SR_THREADS) void k_sweep_rows(Geom g, const bf16x8*
   auto load_tile = [&](int t, int n, St4& v) {
     const uint32_t o = pofs + (uint32_t)(t * H + 32 * n) * 4;
     v.f0 = buf_ld4(rS[1], o); v.g0 = buf_ld4(rS[2], o); v.c0 = buf_ld4(rS[4], o); v.h0 = buf_ld4(rS[5], o);
-    v.cp = buf_ld4<0>(rS[4], o - H * 4);     // c_{t-1}, stored by this thread one t earlier
+    // c_{t-1}, stored by this thread one t earlier: read past the CU's vector L1 (sc0 sc1; a
+    // cached load may return the line as it was before that store -- nondeterministic sweeps)
+    v.cp = buf_ld4<kAuxL2>(rS[4], o - H * 4);
     v.li = buf_ld4(rL[0], o); v.lf = buf_ld4(rL[1], o); v.lg = buf_ld4(rL[2], o);
     v.lo = buf_ld4(rL[3], o); v.lc = buf_ld4(rL[4], o); v.lh = buf_ld4(rL[5], o);
   };
@@ -478,7 +485,16 @@ __global__ __launch_bounds__(SR_THREADS) void k_sweep_rows(Geom g, const bf16x8*
       if (!last) buf_st4<0>(rS[5], po, h1);
       buf_st4(rL[0], po, li); buf_st4(rL[1], po, lf); buf_st4(rL[2], po, lg); buf_st4(rL[3], po, lo);
       buf_st4(rL[4], po, lc);
-      buf_st4(rZ[0], zo4, zi); buf_st4(rZ[1], zo4, zf); buf_st4(rZ[2], zo4, zg); buf_st4(rZ[3], zo4, zo);
+      // one descriptor spans the 4 planes, so its record count cannot drop the stores of rows
+      // past r1 (a ragged last block): they would land in the next plane -- predicate them
+      if (rok) {
+        buf_st4s(rZ, zo4, 0, zi); buf_st4s(rZ, zo4, zpl, zf); buf_st4s(rZ, zo4, 2 * zpl, zg);
+        buf_st4s(rZ, zo4, 3 * zpl, zo);
+      }
+      if (wtgt && rok) {   // same expression as k_resid_gx (IEEE division), so either source gives equal bits
+        buf_st4s(rT, zo4, 0, li / hp.rho[0] + i1); buf_st4s(rT, zo4, zpl, lf / hp.rho[1] + f1);
+        buf_st4s(rT, zo4, 2 * zpl, lg / hp.rho[2] + g1); buf_st4s(rT, zo4, 3 * zpl, lo / hp.rho[3] + o1);
+      }
 #ifdef SR_TIMING
       const unsigned long long tc_ = clock64();
       if ((threadIdx.x & 63) == 0) { sr_comp += tb_ - ta_; sr_store += tc_ - tb_; }
@@ -909,6 +925,9 @@ __device__ __forceinline__ void direct_candidates(float cr, float e, float E, fl
 // make the same sequence of dq_push / dq_run calls (loops below are wave-uniform).
 constexpr int kDQ = 256;   // ring capacity: pending <= 63 before up to two pushes of <= 64 (trial_pair)
 struct DirectQ {
+  // the pushes (ds_write) and the run's reads (ds_read) of other lanes' entries address the same
+  // array, so they stay in program order, and a wave's LDS operations execute in order: no
+  // memory fence (a fence would also order, and so de-scalarise, the caller's global loads)
   float* buf;              // this wave's [5][kDQ] in LDS
   int head, tail;          // wave-uniform counters
 };
@@ -929,9 +948,6 @@ __device__ __forceinline__ void dq_push(DirectQ& dq, bool p, float cr, float e, 
 
 __device__ __forceinline__ void dq_run(DirectQ& dq, float (&acc)[kSlots], bool final) {
   while (dq.tail - dq.head >= 64 || (final && dq.tail > dq.head)) {
-    // the queue is written and read by the lanes of one wave: LDS operations of a wave execute
-    // in order, so a wave barrier (no memory fence: a fence would make every global load of
-    // the caller's loop a clobbered, vector load) orders the pushes before these reads
     __builtin_amdgcn_wave_barrier();
     const int lane = threadIdx.x & 63;
     const int n = dq.tail - dq.head < 64 ? dq.tail - dq.head : 64;
@@ -1310,7 +1326,7 @@ __device__ __forceinline__ void trial_fast_body(const Geom& g, int q, int pass, 
 
 // Wsrc: side 0 -> G_x [4][D][H]; side 1 -> unused (Q holds the h-side direction)
 #ifndef TF_MINB
-#define TF_MINB 3   // workgroups per CU the register allocation must allow (occupancy for the streams)
+#define TF_MINB 1   // workgroups per CU the register allocation must allow (occupancy for the streams)
 #endif
 template <int SIDE, int DP, bool XV, bool UR>
 __global__ __launch_bounds__(kThreads, TF_MINB) void k_trial_fast(Geom g, int pass, const float* zc, const float* tgt,
@@ -1454,7 +1470,7 @@ __global__ __launch_bounds__(kThreads) void k_apply_dwx(Geom g, const float* __r
 // and per block the partial sums X^T R into a [D][H] slab (R never reaches HBM).
 template <int DP, bool XV>
 __global__ __launch_bounds__(kThreads) void k_resid_gx(Geom g, Hyper hp, const float* x, Planes6 S, Planes6 L,
-                                                         const float* zc, float* tgt, float* slab) {
+                                                         const float* zc, float* tgt, float* slab, bool tgt_ready) {
   extern __shared__ float gl[];  // [D][H] block accumulator
   const int q = blockIdx.y;
   const bool th = (q == 2);
@@ -1478,11 +1494,15 @@ __global__ __launch_bounds__(kThreads) void k_resid_gx(Geom g, Hyper hp, const f
       float xr[DP];
       load_xrow<DP, XV>(x, row, g.D, xr);
       const float4 z4 = ld_nt(zq + row * g.H + j);
-      const float4 l4 = ld_nt(Lq + so + j);
-      const float4 s4 = ld_nt(Sq + so + j);
       float4 t4;
-      t4.x = l4.x / rho + s4.x; t4.y = l4.y / rho + s4.y; t4.z = l4.z / rho + s4.z; t4.w = l4.w / rho + s4.w;
-      st_nt(tq + row * g.H + j, t4);
+      if (tgt_ready) {
+        t4 = ld_nt(tq + row * g.H + j);
+      } else {
+        const float4 l4 = ld_nt(Lq + so + j);
+        const float4 s4 = ld_nt(Sq + so + j);
+        t4.x = l4.x / rho + s4.x; t4.y = l4.y / rho + s4.y; t4.z = l4.z / rho + s4.z; t4.w = l4.w / rho + s4.w;
+        st_nt(tq + row * g.H + j, t4);
+      }
       const float zz[4] = {z4.x, z4.y, z4.z, z4.w}, tt[4] = {t4.x, t4.y, t4.z, t4.w};
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
@@ -1907,7 +1927,8 @@ void launch_sweep_t(const Geom& g, int t, const Weights& w, const Hyper& hp, con
 
 bool sweep_rows_ok(const Geom& g) {
   // 32-bit buffer offsets: a [B][T+1][H] plane and a [B*T][H] z-cache plane in bytes
-  return g.H % 32 == 0 && g.H <= 256 && g.D <= 32 && g.B * (int64_t)g.TP() * g.H * 4 < (int64_t)UINT32_MAX;
+  return g.H % 32 == 0 && g.H <= 256 && g.D <= 32 && g.B * (int64_t)g.TP() * g.H * 4 < (int64_t)UINT32_MAX &&
+         4 * g.BT() * g.H * 4 < (int64_t)UINT32_MAX;   // the 4-plane z cache / target descriptors
 }
 
 static int sweep_xc(const Geom& g) { return (g.D + 15) / 16; }
@@ -2048,11 +2069,11 @@ int resid_gx_blocks(const Geom& g) {
 size_t fast_lds(const Geom& g) { return (size_t)((g.D + 3) / 4) * 4 * g.H * sizeof(float); }
 
 void launch_resid_gx(const Geom& g, const Hyper& hp, const float* x, const Planes6& S, const Planes6& L,
-                     const float* zc, float* tgt, float* slab, int nblk, hipStream_t s) {
+                     const float* zc, float* tgt, float* slab, int nblk, bool tgt_ready, hipStream_t s) {
   dim3 grid(nblk, 4);
   with_dp(g, [&](auto dp, auto xv) {
     k_resid_gx<decltype(dp)::value, decltype(xv)::value>
-        <<<grid, kThreads, (size_t)g.D * g.H * sizeof(float), s>>>(g, hp, x, S, L, zc, tgt, slab);
+        <<<grid, kThreads, (size_t)g.D * g.H * sizeof(float), s>>>(g, hp, x, S, L, zc, tgt, slab, tgt_ready);
   });
 }
 

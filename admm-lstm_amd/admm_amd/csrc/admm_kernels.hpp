@@ -88,6 +88,7 @@ struct SweepT {
   const float* x;
   Planes6 S, L;             // [B,T+1,H] each
   float* zc;                // [4][B*T][H]: z cache for the next step's first weight stage
+  float* tgt;               // [4][B*T][H]: lam/rho + S of the updated state (k_sweep_rows; nullable)
   int64_t r0, r1;           // sample rows [r0, r1) of this launch
 };
 void launch_sweep_t(const Geom& g, int t, const Weights& w, const Hyper& hp, const SweepT& a, hipStream_t s);
@@ -146,8 +147,10 @@ void launch_trial_reduce(const Geom& g, int pass, const double* part, int nblk, 
 bool fast_path(const Geom& g);
 int resid_gx_blocks(const Geom& g);
 // x stage: tgt = lam/rho + S (stored) and slab[blk][q][d][j] = sum_rows x[row][d] R_q[row][j]
+// tgt_ready: tgt already holds lam/rho + S of this state (written by the persistent sweep):
+// read instead of S and L, and not rewritten
 void launch_resid_gx(const Geom& g, const Hyper& hp, const float* x, const Planes6& S, const Planes6& L,
-                     const float* zc, float* tgt, float* slab, int nblk, hipStream_t s);
+                     const float* zc, float* tgt, float* slab, int nblk, bool tgt_ready, hipStream_t s);
 // trial pass without a materialised Q (side 0: q = x.G_x) or z (side 1: z = zc + x.dWx)
 void launch_trial_fast(const Geom& g, int side, int pass, const float* zc, const float* tgt, const float* Q,
                        const float* x, const float* Wsrc, const int* found, double* part, int nblk, hipStream_t s);
@@ -155,6 +158,7 @@ int stream_blocks(const Geom& g);   // grid (per gate) of the fast streaming pas
 // H % 256 == 0: the fast trial passes run as row-pair workgroups over H/256 column blocks, and
 // write stream_blocks(g) * H/256 partials per slot (the reduce's nblk)
 bool trial_rows_ok(const Geom& g);
+
 // after the x stage (fast path): zc += X dWx
 void launch_apply_dwx(const Geom& g, const float* x, const float* dW, float* zc, hipStream_t s);
 // h stage A^T R with R computed on the fly from zc (already updated) and tgt (side 1, fast path)

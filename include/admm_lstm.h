@@ -162,6 +162,11 @@ int admm_profile_read(AdmmCtx* ctx, double* ms /* [ADMM_PROF_CLASSES] */, int32_
 int admm_debug_trial(const float* z, const float* tgt, const float* q, int64_t n, int32_t tanh_gate, int32_t kbase,
                      double* out, void* stream);
 
+/* Test hook (synchronous): copy a workspace array of the context to device memory dst.
+   which: 0 = z cache [4][B*T][H], 1 = targets lam/rho + S [4][B*T][H] (valid flag in the
+   return value's sign: 1 if the next x stage will read it, 0 if it will recompute it). */
+int admm_debug_workspace(AdmmCtx* ctx, int32_t which, void* dst, int64_t bytes, void* stream);
+
 /* LSTM.forward / init_gate_variables (blocks/lstm.py:43-46, 65-88) without a context.
    x [B,T,D]; wx/wh/wy as above; out_a [B,O].  If gates_out is non-NULL it holds six
    [B,T+1,H] tensors that receive i,f,g,o,c,h at t >= 1 (their time-0 slices are the

@@ -467,3 +467,36 @@ def test_split3_h_stage_matches_f32_mfma(mods, dev, monkeypatch):
         for q in GATES6:
             d = float((out['1'][k][q] - out['0'][k][q]).abs().max())
             assert d <= 1e-5, (k, q, d)
+
+
+@pytest.mark.parametrize('shape', [(100, 3, 5, 64, 1), (2048, 4, 16, 64, 1)])
+def test_repeated_runs_bit_identical(shape, mods, dev):
+    """The step is deterministic: the same problem stepped from scratch several times gives
+    bit-identical weights and line-search exponents.  (100, ...) has a ragged last row block of
+    the persistent sweep, whose out-of-range rows must not write into the next z-cache plane;
+    both shapes read c_{t-1} back within the sweep (must not see a stale L1 line)."""
+    from blocks.lstm import LSTM
+    from parameters import example_parameter_dictionary
+    admm, _ = mods
+    admm.with_dual_y = False
+    B, T, D, H, O_ = shape
+    g = torch.Generator().manual_seed(3)
+    x = torch.rand(B, T, D, generator=g).to(dev)
+    y = torch.rand(B, O_, generator=g).to(dev)
+    pd = example_parameter_dictionary['YahooFinance']
+    ref = None
+    for _ in range(4):
+        torch.manual_seed(0)
+        m = LSTM(D, H, O_).to(dev)
+        opt = admm.ADMMBasedOptimizer(m, (x, y), pd, verbose=False)
+        ks = []
+        for _ in range(3):
+            opt.step()
+            ks.append(list(opt.last_step_stats()['k'].values()))
+        W = torch.cat([p.detach().flatten() for p in m.parameters()])
+        assert torch.isfinite(W).all()
+        if ref is None:
+            ref = (W, ks)
+        else:
+            assert ks == ref[1]
+            assert torch.equal(W, ref[0])

@@ -120,7 +120,7 @@ int main(int argc, char** argv) {
   }
   if (mode == "tr") return 0;
   timeit("trial generic", f4 * 3 * 4 * n, 0, [&] { launch_trial(g, 0, zc, tgt, Q, found, part, trial_blocks(g), s); });
-  timeit("resid_gx", f4 * 4 * 4 * n, 0, [&] { launch_resid_gx(g, hp, x, S, L, zc, tgt, slab, resid_gx_blocks(g), s); });
+  timeit("resid_gx", f4 * 4 * 4 * n, 0, [&] { launch_resid_gx(g, hp, x, S, L, zc, tgt, slab, resid_gx_blocks(g), false, s); });
   const int ns = atr_splits(g, 1);
   timeit("atr_fused", f4 * (2 * 4 * n + BT * g.H), 2.0 * BT * g.H * 4 * g.H,
          [&] { launch_atr_fused(g, hp, x, S.p[5], zc, tgt, dW, slab, ns, s); });
@@ -128,7 +128,7 @@ int main(int argc, char** argv) {
          [&] { launch_atr(g, 1, x, S.p[5], R, slab, ns, s); });
   timeit("qgemm side1", f4 * (4 * n + BT * g.H), 2.0 * BT * g.H * 4 * g.H, [&] { launch_qgemm(g, 1, x, S.p[5], G, Q, s); });
   run_s3();
-  SweepT sw{x, S, L, zc, 0, g.B};
+  SweepT sw{x, S, L, zc, nullptr, 0, g.B};
   timeit("sweep_t (t=5)", f4 * g.B * (g.D + 27.0 * g.H), 2.0 * g.B * (g.D + g.H) * 4 * g.H,
          [&] { launch_sweep_t(g, 5, w, hp, sw, s); });
   {

@@ -500,3 +500,34 @@ def test_repeated_runs_bit_identical(shape, mods, dev):
         else:
             assert ks == ref[1]
             assert torch.equal(W, ref[0])
+
+
+@pytest.mark.parametrize('shape', [(100, 3, 5, 64), (2048, 4, 16, 64), (300, 3, 16, 256)])
+def test_z_cache_matches_recompute(shape, mods, dev):
+    """After a step the z cache (written by the sweep, read by the next step's x stage) equals
+    X_t Wx + h_{t-1} Wh of the new state and weights, to f32-product accuracy."""
+    from admm_amd import _native as N
+    from blocks.lstm import LSTM
+    from parameters import example_parameter_dictionary
+    admm, _ = mods
+    admm.with_dual_y = False
+    B, T, D, H = shape
+    g = torch.Generator().manual_seed(5)
+    x = torch.rand(B, T, D, generator=g).to(dev)
+    y = torch.rand(B, 1, generator=g).to(dev)
+    torch.manual_seed(0)
+    m = LSTM(D, H, 1).to(dev)
+    opt = admm.ADMMBasedOptimizer(m, (x, y), example_parameter_dictionary['GoogleStock'], verbose=False)
+    for _ in range(2):
+        opt.step()
+    buf = torch.empty(4, B * T, H, device=dev)
+    lib = N.load()
+    valid = lib.admm_debug_workspace(opt._ctx, 0, N.ptr(buf), buf.numel() * 4, N.stream_handle(dev))
+    assert valid == 1
+    hp = opt.gates['h'][:, :T, :].reshape(B * T, H).double()
+    X = x.reshape(B * T, D).double()
+    for qi, q in enumerate('ifgo'):
+        wx, wh = getattr(m, f'x2{q}').detach().double(), getattr(m, f'h2{q}').detach().double()
+        ref = X @ wx + hp @ wh
+        scale = (X.abs() @ wx.abs() + hp.abs() @ wh.abs()).max().item()
+        assert float((buf[qi].double() - ref).abs().max()) <= 1e-5 * scale, q

@@ -185,7 +185,6 @@ int stage_weights(AdmmCtx* c, int side, hipStream_t s) {
   const int Kd = side == 0 ? g.D : g.H;
   const bool fast = fast_path(g) && !c->force_generic;
   const Planes6 S = planes(c->buf.gates), L = planes(c->buf.duals);
-  HIP_TRY(hipMemsetAsync(c->found, 0, 4 * sizeof(int), s));
   if (fast && side == 1) {  // z of the h-side searches uses the updated x2q (admm.py:298-300)
     ProfScope ps(c, ADMM_PROF_RESID, s);
     launch_apply_dwx(g, c->buf.x, c->dW, c->zc, s);
@@ -223,7 +222,7 @@ int stage_weights(AdmmCtx* c, int side, hipStream_t s) {
     ProfScope ps(c, side == 0 ? ADMM_PROF_ATR_X : ADMM_PROF_ATR_H, s);
     launch_atr(g, side, c->buf.x, c->buf.gates[ADMM_H], c->R, c->gslab, ns, s);
   }
-  launch_reduce_g(g, side, c->hp, c->gslab, ns, c->G, s);
+  launch_reduce_g(g, side, c->hp, c->gslab, ns, c->G, c->found, s);
   int rc = allreduce_f32(c, c->G, (size_t)4 * Kd * g.H, s);
   if (rc) return rc;
   // 2. trial direction Q = A G (not needed on the fast x side: formed inside the trials)

@@ -432,6 +432,9 @@ __global__ __launch_bounds__(SR_THREADS) void k_sweep_rows(Geom g, const bf16x8*
     }
   };
 
+  // Tile operands are loaded one tile early.  A tile's c_{t-1} is stored NT tiles before its own
+  // step, so the read-back needs NT > 1 (loading two tiles ahead measured no faster).
+  static_assert(NT > 1, "c_{t-1} read-back needs the store NT tiles earlier");
   St4 nxt;
   load_tile(1, 0, nxt);
   load_x(2);                 // step 0: the producer computes tile (1, 0)
@@ -804,9 +807,10 @@ __global__ __launch_bounds__(kThreads) void k_atr_fused(Geom g, const float* x, 
 }
 
 __global__ __launch_bounds__(kThreads) void k_reduce_g(int Kd, int H, Hyper hp, const float* slab, int nsplit,
-                                                         float* G) {
+                                                         float* G, int* found) {
   const int64_t per_q = (int64_t)Kd * H;
   const int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+  if (i < 4) found[i] = 0;   // this stage's line searches start undecided (no memset launch)
   if (i >= 4 * per_q) return;
   const int q = (int)(i / per_q);
   double s = 0.0;
@@ -1927,7 +1931,8 @@ void launch_sweep_t(const Geom& g, int t, const Weights& w, const Hyper& hp, con
 
 bool sweep_rows_ok(const Geom& g) {
   // 32-bit buffer offsets: a [B][T+1][H] plane and a [B*T][H] z-cache plane in bytes
-  return g.H % 32 == 0 && g.H <= 256 && g.D <= 32 && g.B * (int64_t)g.TP() * g.H * 4 < (int64_t)UINT32_MAX &&
+  // H >= 64: a tile's c_{t-1} is read back from the state plane, stored NT = H/32 tiles earlier
+  return g.H % 32 == 0 && g.H >= 64 && g.H <= 256 && g.D <= 32 && g.B * (int64_t)g.TP() * g.H * 4 < (int64_t)UINT32_MAX &&
          4 * g.BT() * g.H * 4 < (int64_t)UINT32_MAX;   // the 4-plane z cache / target descriptors
 }
 
@@ -1948,7 +1953,7 @@ static void launch_sweep_rows_xc(const Geom& g, const bf16x8* wt, const Hyper& h
   dim3 grid(cdiv64(a.r1 - a.r0, SR_ROWS));
   switch (g.H / 32) {
 #define SR_CASE(N) case N: k_sweep_rows<N, XC><<<grid, SR_THREADS, 0, s>>>(g, wt, hp, a); break;
-    SR_CASE(1) SR_CASE(2) SR_CASE(3) SR_CASE(4) SR_CASE(5) SR_CASE(6) SR_CASE(7) SR_CASE(8)
+    SR_CASE(2) SR_CASE(3) SR_CASE(4) SR_CASE(5) SR_CASE(6) SR_CASE(7) SR_CASE(8)
 #undef SR_CASE
     default: break;
   }
@@ -2016,11 +2021,11 @@ void launch_atr(const Geom& g, int side, const float* x, const float* Sh, const 
   }
 }
 
-void launch_reduce_g(const Geom& g, int side, const Hyper& hp, const float* slab, int nsplit, float* G,
+void launch_reduce_g(const Geom& g, int side, const Hyper& hp, const float* slab, int nsplit, float* G, int* found,
                      hipStream_t s) {
   const int Kd = side == 0 ? g.D : g.H;
   const int64_t n = 4LL * Kd * g.H;
-  k_reduce_g<<<cdiv64(n, kThreads), kThreads, 0, s>>>(Kd, g.H, hp, slab, nsplit, G);
+  k_reduce_g<<<cdiv64(n, kThreads), kThreads, 0, s>>>(Kd, g.H, hp, slab, nsplit, G, found);
 }
 
 void launch_qgemm(const Geom& g, int side, const float* x, const float* Sh, const float* G, float* Q,

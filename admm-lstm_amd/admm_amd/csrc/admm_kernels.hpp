@@ -125,8 +125,8 @@ void launch_resid(const Geom& g, const Hyper& hp, const ResidArgs& a, hipStream_
 int atr_splits(const Geom& g, int side);
 void launch_atr(const Geom& g, int side, const float* x, const float* Sh, const float* R, float* Gslab,
                 int nsplit, hipStream_t s);
-// G[q][m][j] = rho_q * sum_split Gslab
-void launch_reduce_g(const Geom& g, int side, const Hyper& hp, const float* Gslab, int nsplit, float* G,
+// G[q][m][j] = rho_q * sum_split Gslab; also clears found[0..3] for the stage's line searches
+void launch_reduce_g(const Geom& g, int side, const Hyper& hp, const float* Gslab, int nsplit, float* G, int* found,
                      hipStream_t s);
 // Q[q][row][j] = sum_m A[row][m] * G[q][m][j]
 void launch_qgemm(const Geom& g, int side, const float* x, const float* Sh, const float* G, float* Q,

@@ -307,7 +307,7 @@ def test_forward_matches_oracle(dev):
 
 
 @pytest.mark.parametrize('shape', [(200, 5, 3, 40, 2), (33, 1, 2, 7, 1), (129, 4, 5, 33, 3),
-                                   (100, 3, 5, 64, 1), (40, 1, 16, 32, 1)])
+                                   (100, 3, 5, 64, 1), (40, 1, 16, 32, 1), (64, 3, 4, 32, 1), (70, 3, 2, 96, 1)])
 def test_edge_shapes_vs_oracle(shape, mods, dev):
     """Ragged tiles (B, H not multiples of 128/32), T = 1, multi-output O.  H % 32 == 0 runs the
     persistent sweep (k_sweep_rows) with a ragged last row block; the others the per-t sweep."""

@@ -173,6 +173,9 @@ int atr3_splits(const Geom& g);
 void launch_atr3(const Geom& g, const float* Sh, const float* zc, const float* tgt, float* slab, int nsplit,
                  hipStream_t s);
 void launch_qgemm3(const Geom& g, const float* Sh, const float* G, float* gimg, float* Q, hipStream_t s);
+// the two halves of launch_qgemm3: G -> split image, then Q = Hprev G (gates with found[q] set skipped)
+void launch_split_g(const Geom& g, const float* G, float* gimg, hipStream_t s);
+void launch_qgemm3_img(const Geom& g, const float* Sh, const float* gimg, float* Q, const int* found, hipStream_t s);
 // decide the first passing k in this pass's window; on success update the weights
 struct SelectArgs {
   int side;                 // 0 x, 1 h

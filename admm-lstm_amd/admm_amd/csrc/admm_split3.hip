@@ -19,45 +19,10 @@
 // swapped when ((r >> 2) ^ (r >> 3)) & 1.  Fragment reads (32 consecutive rows per half-wave, one
 // half) and staging writes (8 consecutive lanes on 8 consecutive rows, one half; or 4 rows x 2
 // halves) are then conflict-free under the gfx950 bank rules (MI355X_MICROARCH.md §LDS).
-#include "admm_dev.hpp"
-#include "admm_kernels.hpp"
+#include "admm_split3.hpp"
 
 namespace admm {
 namespace {
-
-typedef float f32x8 __attribute__((ext_vector_type(8)));
-
-#ifndef S3_ABL
-#define S3_ABL 0   // kernel ablations for tools/kbench (bitmask, 0 = full kernels)
-#endif
-
-__device__ __forceinline__ int sw_off(int r, int h) {   // bf16 offset of half h of row r
-  return r * 16 + 8 * (h ^ (((r >> 2) ^ (r >> 3)) & 1));
-}
-
-// the six piece products, smallest first: (a2 b0, a1 b1, a0 b2, a1 b0, a0 b1, a0 b0)
-__device__ __forceinline__ f32x16 mfma_split3(const bf16x8 (&a)[3], const bf16x8 (&b)[3], f32x16 acc) {
-  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[2], b[0], acc, 0, 0, 0);
-  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], b[1], acc, 0, 0, 0);
-  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[2], acc, 0, 0, 0);
-  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], b[0], acc, 0, 0, 0);
-  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[1], acc, 0, 0, 0);
-  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[0], acc, 0, 0, 0);
-  return acc;
-}
-
-__device__ __forceinline__ void frag3(const __bf16* img, int piece_stride, int off, bf16x8 (&f)[3]) {
-#pragma unroll
-  for (int p = 0; p < 3; ++p) f[p] = *reinterpret_cast<const bf16x8*>(img + p * piece_stride + off);
-}
-
-__device__ __forceinline__ void put3(__bf16* img, int piece_stride, int off, f32x8 v) {
-  bf16x8 p0, p1, p2;
-  split3(v, p0, p1, p2);
-  *reinterpret_cast<bf16x8*>(img + off) = p0;
-  *reinterpret_cast<bf16x8*>(img + piece_stride + off) = p1;
-  *reinterpret_cast<bf16x8*>(img + 2 * piece_stride + off) = p2;
-}
 
 // ------------------------------------------------------------------ G image for k_qgemm3
 // gi[(((q * NK + c) * NTT + n) * 3 + p) * 64 + lane] = piece p of G_q[16c + 8(lane>>5) + e][32n + (lane&31)],
@@ -81,73 +46,23 @@ __global__ __launch_bounds__(kThreads) void k_split_g(int H, const float* __rest
 }
 
 // ------------------------------------------------------------------ Q = Hprev G
-// Workgroup: 128 rows x 256 columns of one gate (H % 256 == 0), 4 waves as 2 (rows) x 2
-// (columns) of 64 x 128; K = H in 16-deep steps through double-buffered LDS, the global loads
-// of step c+1 in flight during the MFMAs of step c.
-constexpr int Q3_BM = 128, Q3_BN = 256;
-
+// One 128 x 256 tile of one gate per workgroup (qgemm3_tile).  found != nullptr: gates whose
+// line search has already decided are skipped (the later trial passes, when pass 0 ran fused
+// in k_qtrial3 and Q was never formed).
 __global__ __launch_bounds__(kThreads) void k_qgemm3(Geom g, const float* __restrict__ Sh,
-                                                      const bf16x8* __restrict__ gi, float* __restrict__ Q) {
-  constexpr int AP = Q3_BM * 16;            // one piece of the A image (bf16)
-  constexpr int BU = (Q3_BN / 32) * 3 * 64; // bf16x8 units of one B step image
-  __shared__ __attribute__((aligned(16))) __bf16 As[2][3 * AP];
-  __shared__ bf16x8 Bs[2][BU];
-  const int H = g.H, NK = H / 16, NTT = H / 32, ncb = H / Q3_BN;
+                                                      const bf16x8* __restrict__ gi, float* __restrict__ Q,
+                                                      const int* __restrict__ found) {
+  __shared__ __attribute__((aligned(16))) char lds[kQ3Lds];
+  const int H = g.H, ncb = H / Q3_BN;
   int lid = xcd_swizzle(blockIdx.x, gridDim.x);
   const int cb = lid % ncb;
   lid /= ncb;
   const int q = lid % 4;
+  if (found && found[q]) return;
   const int64_t m0 = (int64_t)(lid / 4) * Q3_BM, BT = g.BT();
-  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  // staging: thread = (row sr, k-half sh) of A; 6 units of the B image
-  const int sr = tid >> 1, sh = tid & 1;
-  const int64_t arow = m0 + sr < BT ? m0 + sr : BT - 1;   // rows past BT: computed, not stored
-  const float* ap = Sh + g.hrow(arow) * H + 8 * sh;
-  const bf16x8* bp = gi + ((size_t)q * NK * NTT + (size_t)(Q3_BN / 32) * cb) * 192 + tid;
-  const size_t bstep = (size_t)NTT * 192;
-  float4 ra0, ra1;
-  bf16x8 rb[BU / kThreads];
-  auto gload = [&](int c) {
-    if (S3_ABL & 32) {
-      ra0 = make_float4(c, 1.f, 2.f, 3.f); ra1 = ra0;
-    } else {
-      ra0 = *reinterpret_cast<const float4*>(ap + 16 * c);
-      ra1 = *reinterpret_cast<const float4*>(ap + 16 * c + 4);
-    }
-#pragma unroll
-    for (int u = 0; u < BU / kThreads; ++u) rb[u] = bp[c * bstep + u * kThreads];
-  };
-  auto lstore = [&](int st) {
-    put3(As[st], AP, sw_off(sr, sh), f32x8{ra0.x, ra0.y, ra0.z, ra0.w, ra1.x, ra1.y, ra1.z, ra1.w});
-#pragma unroll
-    for (int u = 0; u < BU / kThreads; ++u) Bs[st][tid + u * kThreads] = rb[u];
-  };
-  const int wr = wave >> 1, wc = wave & 1, c32 = lane & 31, kh = lane >> 5;
   f32x16 acc[2][4];
-  zero_acc(acc);
-  gload(0);
-  lstore(0);
-  __syncthreads();
-  for (int c = 0; c < NK; ++c) {
-    const int st = c & 1;
-    if (c + 1 < NK) gload(c + 1);
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int mi = 0; mi < 2; ++mi) {
-      bf16x8 a[3];
-      frag3(As[st], AP, sw_off(wr * 64 + mi * 32 + c32, kh), a);
-#pragma unroll
-      for (int ni = 0; ni < 4; ++ni) {
-        const bf16x8* bb = &Bs[st][(wc * 4 + ni) * 192 + lane];
-        const bf16x8 b[3] = {bb[0], bb[64], bb[128]};
-        if (S3_ABL & 64) acc[mi][ni][0] += (float)a[0][0] * (float)b[0][0];
-        else acc[mi][ni] = mfma_split3(a, b, acc[mi][ni]);
-      }
-    }
-    __builtin_amdgcn_sched_barrier(0);
-    if (c + 1 < NK) lstore(st ^ 1);
-    __syncthreads();
-  }
+  qgemm3_tile(g, Sh, gi, q, cb, m0, lds, acc);
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, wr = wave >> 1, wc = wave & 1, c32 = lane & 31;
   float* Qq = Q + (int64_t)q * BT * H + Q3_BN * cb + wc * 128 + c32;
 #pragma unroll
   for (int mi = 0; mi < 2; ++mi)
@@ -162,126 +77,160 @@ __global__ __launch_bounds__(kThreads) void k_qgemm3(Geom g, const float* __rest
 }
 
 // ------------------------------------------------------------------ slab = Hprev^T R
-// Workgroup: 256 hidden units m x 256 columns j of one gate (H % 256 == 0) over the rows of one
-// split, in 16-row steps; 4 waves as 2 (m) x 2 (j) of 128 x 128 (256 accumulators per lane),
-// one wave per SIMD.  Both MFMA operands are k(= row)-strided in memory.  Staging keeps rows as
-// they are: a thread loads 4 rows x 4 columns (float4, a wave-instruction = one 1-KB row) and
+// Workgroup: 256 hidden units m x BN columns j of one gate (H % 256 == 0) over the rows of one
+// split, in 16-row steps; 4 waves as 2 (m) x 2 (j) of 128 x BN/2.  BN = 256: 256 accumulators
+// per lane, one workgroup (one wave per SIMD) per CU.  BN = 128: 128 accumulators, 72 KB of LDS,
+// two workgroups per CU so one wave's MFMAs overlap the other's loads and split arithmetic.
+// Both MFMA operands are k(= row)-strided in memory.  Staging keeps rows as they are: a thread
+// loads float4s of whole rows (a wave-instruction = one 1-KB Hprev row, one or two rows of R) and
 // stores the split pieces row-major; the fragments come back transposed through
 // ds_read_b64_tr_b16 (two per piece: rows k..k+3 and k+4..k+7 of 16 columns per lane group).
-// Images: [piece][half of the columns][16 rows][128 bf16], 256-B rows whose 16-B chunks are
+// Images: [piece][128-column block][16 rows][128 bf16], 256-B rows whose 16-B chunks are
 // XOR-permuted by the row (cdna_hip_programming.md T10 image (b)): the row-major staging writes
 // and the transposed reads are both conflict-free.  The loads run two steps ahead through a
 // two-slot register ring.
-constexpr int A3_BM = 256, A3_BN = 256, A3_KS = 16;
-constexpr int A3_SUB = A3_KS * 128;          // bf16 of one half-image (16 rows x 128 columns)
-constexpr int A3_PIECE = 2 * A3_SUB;         // one split piece of one operand
-constexpr int A3_OPER = 3 * A3_PIECE;        // one operand (A or R) of one stage
-constexpr int A3_STAGE = 2 * A3_OPER;
+#ifndef A3_BN_SEL
+#define A3_BN_SEL 256   // 128: two workgroups per CU (measured slower on C3: 1.10 vs 1.05 ms)
+#endif
+constexpr int A3_BM = 256, A3_BN = A3_BN_SEL, A3_KS = 16;
+constexpr int A3_SUB = A3_KS * 128;          // bf16 of one 128-column block (16 rows x 128 columns)
+
+template <int BN>
+struct A3 {
+  static constexpr int PA = (A3_BM / 128) * A3_SUB;   // one split piece of the Hprev operand
+  static constexpr int PR = (BN / 128) * A3_SUB;      // one split piece of the R operand
+  static constexpr int STAGE = 3 * PA + 3 * PR;
+  static constexpr int LPR = BN / 4;                   // lanes per R row (float4 each)
+  static constexpr int RPI = 64 / LPR;                 // R rows per wave-instruction
+  static constexpr int NR = 4 / RPI;                   // R loads per thread per step
+  static constexpr int NI = BN / 64;                   // 32-column fragments per wave
+  static constexpr int MINB = BN == 128 ? 2 : 1;       // workgroups per CU
+};
 
 __device__ __forceinline__ int a3_off(int row, int col) {   // bf16 offset of (row, col), col % 4 == 0
   const int sub = col >> 7, cw = col & 127, ch = cw >> 3;
   return sub * A3_SUB + row * 128 + 8 * (ch ^ (((row & 3) << 2) | ((row >> 2) & 3))) + (cw & 4);
 }
 
-struct Atr3Ring { float4 a[4], z[4], t[4]; };
+template <int BN>
+struct Atr3Ring { float4 a[4], z[A3<BN>::NR], t[A3<BN>::NR]; };
 
-template <bool TANH>
+template <bool TANH, int BN>
 __device__ __forceinline__ void atr3_body(const Geom& g, int mb, int nb, int q, int sp, int nsplit,
                                           const float* __restrict__ Sh, const float* __restrict__ zq,
                                           const float* __restrict__ tq, float* __restrict__ slab, __bf16* img) {
+  using P = A3<BN>;
   const int H = g.H;
   const int64_t BT = g.BT();
   const int64_t per = ((BT + nsplit - 1) / nsplit + A3_KS - 1) / A3_KS * A3_KS;
   const int64_t r0 = sp * per, r1 = r0 + per < BT ? r0 + per : BT;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  // staging: columns 4cg..4cg+3, rows 4rg..4rg+3 of a step; rg (the wave) made provably uniform
-  // so the row offsets stay in SGPRs (no waterfall loops around the buffer loads, guide T20)
+  // staging: Hprev columns 4cg..4cg+3 of rows 4rg..4rg+3; R columns 4cz.. of rows
+  // 4rg + RPI i + lh.  rg (the wave) is made provably uniform so the row offsets stay in SGPRs
+  // (no waterfall loops around the buffer loads, guide T20)
   const int cg = lane, rg = __builtin_amdgcn_readfirstlane(wave);
+  const int lh = lane / P::LPR, cz = lane % P::LPR;
   const __amdgpu_buffer_rsrc_t rA = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(Sh), 0,
                                                                       (int)(g.B * g.TP() * H * 4), kBufWord3);
   const __amdgpu_buffer_rsrc_t rZ = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(zq), 0, (int)(BT * H * 4), kBufWord3);
   const __amdgpu_buffer_rsrc_t rT = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(tq), 0, (int)(BT * H * 4), kBufWord3);
-  const int va = (mb * A3_BM + 4 * cg) * 4, vz = (nb * A3_BN + 4 * cg) * 4;
+  const int va = (mb * A3_BM + 4 * cg) * 4, vz = (nb * BN + 4 * cz) * 4;
   // rows past r1 are loaded clamped (branch-free) and meet R = 0 in put()
-  auto gload = [&](Atr3Ring& R, int64_t k0) {
+  auto gload = [&](Atr3Ring<BN>& R, int64_t k0) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int64_t r = k0 + 4 * rg + i, row = r < r1 ? r : r1 - 1;
-      const int sa = (int)(g.hrow(row) * H * 4), sz = (int)(row * H * 4);
+      const int sa = (int)(g.hrow(row) * H * 4);
       R.a[i] = (S3_ABL & 1) ? make_float4(i, 1, 2, 3)
                             : __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rA, va, sa, 0));
+    }
+#pragma unroll
+    for (int i = 0; i < P::NR; ++i) {
+      int vo = vz, so = 0;
+      if constexpr (P::RPI == 1) {
+        const int64_t r = k0 + 4 * rg + i, row = r < r1 ? r : r1 - 1;
+        so = (int)(row * H * 4);
+      } else {   // the row depends on the lane: the offset goes into the VGPR
+        const int64_t r = k0 + 4 * rg + P::RPI * i + lh, row = r < r1 ? r : r1 - 1;
+        vo += (int)row * H * 4;
+      }
       R.z[i] = (S3_ABL & 2) ? make_float4(0.1f, 0.2f, 0.3f, 0.4f)
-                            : __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rZ, vz, sz, 2));
+                            : __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rZ, vo, so, 2));
       R.t[i] = (S3_ABL & 2) ? make_float4(0.5f, 0.5f, 0.5f, 0.5f)
-                            : __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rT, vz, sz, 2));
+                            : __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rT, vo, so, 2));
     }
   };
-  // split row i of a ring slot (4 columns of Hprev and of R) into the images of stage st
-  auto put_row = [&](int st, const Atr3Ring& R, int64_t k0, int i) {
-    __bf16* A = img + st * A3_STAGE;
-    __bf16* B = A + A3_OPER;
-    const int o = a3_off(4 * rg + i, 4 * cg);
-    const bool ok = k0 + 4 * rg + i < r1;
-    const float zz[4] = {R.z[i].x, R.z[i].y, R.z[i].z, R.z[i].w};
-    const float tt[4] = {R.t[i].x, R.t[i].y, R.t[i].z, R.t[i].w};
-    f32x4 rv;
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      float phi, dphi;
-      phi_fast<TANH>(zz[u], phi, dphi);
-      rv[u] = ok ? (phi - tt[u]) * dphi : 0.f;
-    }
+  // split a ring slot (4 columns of 4 Hprev rows and of NR R rows) into the images of stage st
+  auto put = [&](int st, const Atr3Ring<BN>& R, int64_t k0) {
+    __bf16* A = img + st * P::STAGE;
+    __bf16* B = A + 3 * P::PA;
     bf16x4 p0, p1, p2;
-    split3(f32x4{R.a[i].x, R.a[i].y, R.a[i].z, R.a[i].w}, p0, p1, p2);
-    *reinterpret_cast<bf16x4*>(A + o) = p0;
-    *reinterpret_cast<bf16x4*>(A + A3_PIECE + o) = p1;
-    *reinterpret_cast<bf16x4*>(A + 2 * A3_PIECE + o) = p2;
-    split3(rv, p0, p1, p2);
-    *reinterpret_cast<bf16x4*>(B + o) = p0;
-    *reinterpret_cast<bf16x4*>(B + A3_PIECE + o) = p1;
-    *reinterpret_cast<bf16x4*>(B + 2 * A3_PIECE + o) = p2;
-  };
-  auto put = [&](int st, const Atr3Ring& R, int64_t k0) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) put_row(st, R, k0, i);
+    for (int i = 0; i < 4; ++i) {
+      const int o = a3_off(4 * rg + i, 4 * cg);
+      split3(f32x4{R.a[i].x, R.a[i].y, R.a[i].z, R.a[i].w}, p0, p1, p2);
+      *reinterpret_cast<bf16x4*>(A + o) = p0;
+      *reinterpret_cast<bf16x4*>(A + P::PA + o) = p1;
+      *reinterpret_cast<bf16x4*>(A + 2 * P::PA + o) = p2;
+    }
+#pragma unroll
+    for (int i = 0; i < P::NR; ++i) {
+      const int rr = 4 * rg + P::RPI * i + lh;
+      const int o = a3_off(rr, 4 * cz);
+      const bool ok = k0 + rr < r1;
+      const float zz[4] = {R.z[i].x, R.z[i].y, R.z[i].z, R.z[i].w};
+      const float tt[4] = {R.t[i].x, R.t[i].y, R.t[i].z, R.t[i].w};
+      f32x4 rv;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        float phi, dphi;
+        phi_fast<TANH>(zz[u], phi, dphi);
+        rv[u] = ok ? (phi - tt[u]) * dphi : 0.f;
+      }
+      split3(rv, p0, p1, p2);
+      *reinterpret_cast<bf16x4*>(B + o) = p0;
+      *reinterpret_cast<bf16x4*>(B + P::PR + o) = p1;
+      *reinterpret_cast<bf16x4*>(B + 2 * P::PR + o) = p2;
+    }
   };
   // transposed fragment reads: lane group gi = lane >> 4 takes columns +16 (gi & 1) and rows
   // 8 (gi >> 1) .. +7; lane 4qq + pp of a group addresses row qq (+4 for the second read),
   // columns 4pp..4pp+3
   const int gi = lane >> 4, qq = (lane >> 2) & 3, pp = lane & 3;
   const int frow = 8 * (gi >> 1) + qq, fcol = 16 * (gi & 1) + 4 * pp;
-  auto frag = [&](const __bf16* O, int cbase, bf16x8 (&f)[3]) {
+  auto frag = [&](const __bf16* O, int piece, int cbase, bf16x8 (&f)[3]) {
     const int o0 = a3_off(frow, cbase + fcol), o1 = a3_off(frow + 4, cbase + fcol);
 #pragma unroll
     for (int p = 0; p < 3; ++p) {
       typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
-      const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(O + p * A3_PIECE + o0));
-      const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(O + p * A3_PIECE + o1));
+      const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(O + p * piece + o0));
+      const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(O + p * piece + o1));
       f[p] = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
     }
   };
   const int wr = wave >> 1, wc = wave & 1;
-  f32x16 acc[4][4];
+  f32x16 acc[4][P::NI];
   zero_acc(acc);
   auto compute = [&](int st) {
-    const __bf16* A = img + st * A3_STAGE;
-    const __bf16* B = A + A3_OPER;
-    bf16x8 b[4][3];
+    const __bf16* A = img + st * P::STAGE;
+    const __bf16* B = A + 3 * P::PA;
+    bf16x8 b[P::NI][3];
 #pragma unroll
-    for (int ni = 0; ni < 4; ++ni) frag(B, wc * 128 + ni * 32, b[ni]);
+    for (int ni = 0; ni < P::NI; ++ni) frag(B, P::PR, wc * (BN / 2) + ni * 32, b[ni]);
 #pragma unroll
     for (int mi = 0; mi < 4; ++mi) {
       bf16x8 a[3];
-      frag(A, wr * 128 + mi * 32, a);
+      frag(A, P::PA, wr * 128 + mi * 32, a);
 #pragma unroll
-      for (int ni = 0; ni < 4; ++ni) {
+      for (int ni = 0; ni < P::NI; ++ni) {
         if (S3_ABL & 4) acc[mi][ni][0] += (float)a[0][0] * (float)b[ni][0][0];
         else acc[mi][ni] = mfma_split3(a, b[ni], acc[mi][ni]);
       }
     }
   };
-  if (r0 < r1) {
-    Atr3Ring R0, R1;
+  if (r0 >= r1) {
+  } else if constexpr (P::MINB == 1) {
+    Atr3Ring<BN> R0, R1;
     gload(R0, r0);
     gload(R1, r0 + A3_KS);
     put(0, R0, r0);
@@ -298,21 +247,38 @@ __device__ __forceinline__ void atr3_body(const Geom& g, int mb, int nb, int q, 
       put(0, R0, k0 + 2 * A3_KS);
       __syncthreads();
     }
+  } else {
+    // two workgroups per CU: a one-slot ring (step s+1 in flight during the MFMAs of step s);
+    // the other workgroup covers the rest of the load latency
+    Atr3Ring<BN> R0;
+    gload(R0, r0);
+    put(0, R0, r0);
+    __syncthreads();
+    int st = 0;
+    for (int64_t k0 = r0; k0 < r1; k0 += A3_KS) {
+      gload(R0, k0 + A3_KS);
+      compute(st);
+      put(st ^ 1, R0, k0 + A3_KS);
+      __syncthreads();
+      st ^= 1;
+    }
   }
-  float* out = slab + ((int64_t)sp * 4 + q) * H * H + nb * A3_BN + wc * 128 + (lane & 31);
+  float* out = slab + ((int64_t)sp * 4 + q) * H * H + nb * BN + wc * (BN / 2) + (lane & 31);
 #pragma unroll
   for (int mi = 0; mi < 4; ++mi)
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int m = mb * A3_BM + wr * 128 + mi * 32 + acc_row(r, lane);
 #pragma unroll
-      for (int ni = 0; ni < 4; ++ni) out[(int64_t)m * H + ni * 32] = acc[mi][ni][r];
+      for (int ni = 0; ni < P::NI; ++ni) out[(int64_t)m * H + ni * 32] = acc[mi][ni][r];
     }
 }
 
-__global__ __launch_bounds__(kThreads) void k_atr3(Geom g, const float* __restrict__ Sh, const float* __restrict__ zc,
-                                                    const float* __restrict__ tgt, float* __restrict__ slab, int nsplit) {
-  __shared__ __attribute__((aligned(16))) __bf16 img[2 * A3_STAGE];
+__global__ __launch_bounds__(kThreads, A3<A3_BN>::MINB) void k_atr3(Geom g, const float* __restrict__ Sh,
+                                                                     const float* __restrict__ zc,
+                                                                     const float* __restrict__ tgt,
+                                                                     float* __restrict__ slab, int nsplit) {
+  __shared__ __attribute__((aligned(16))) __bf16 img[2 * A3<A3_BN>::STAGE];
   const int nmb = g.H / A3_BM, nnb = g.H / A3_BN;
   int lid = xcd_swizzle(blockIdx.x, gridDim.x);
   const int q = lid % 4;          // the 4 gates of one split share the Hprev rows: same XCD
@@ -322,9 +288,9 @@ __global__ __launch_bounds__(kThreads) void k_atr3(Geom g, const float* __restri
   const int nb = lid % nnb, sp = lid / nnb;
   const int64_t n = g.BT() * g.H;
   if (q == 2)
-    atr3_body<true>(g, mb, nb, q, sp, nsplit, Sh, zc + q * n, tgt + q * n, slab, img);
+    atr3_body<true, A3_BN>(g, mb, nb, q, sp, nsplit, Sh, zc + q * n, tgt + q * n, slab, img);
   else
-    atr3_body<false>(g, mb, nb, q, sp, nsplit, Sh, zc + q * n, tgt + q * n, slab, img);
+    atr3_body<false, A3_BN>(g, mb, nb, q, sp, nsplit, Sh, zc + q * n, tgt + q * n, slab, img);
 }
 
 }  // namespace
@@ -337,7 +303,7 @@ size_t split3_gimg_floats(const Geom& g) { return (size_t)4 * g.H * g.H * 3 / 2;
 
 int atr3_splits(const Geom& g) {
   const int tiles = (g.H / A3_BM) * (g.H / A3_BN) * 4;
-  int ns = 256 / tiles;                     // one resident wave of workgroups (1 per CU)
+  int ns = 256 * A3<A3_BN>::MINB / tiles;   // one resident wave of workgroups
   const int64_t max_by_rows = g.BT() / 256;
   if (ns > max_by_rows) ns = (int)max_by_rows;
   return ns < 1 ? 1 : ns;
@@ -349,13 +315,20 @@ void launch_atr3(const Geom& g, const float* Sh, const float* zc, const float* t
   k_atr3<<<grid, kThreads, 0, s>>>(g, Sh, zc, tgt, slab, nsplit);
 }
 
-void launch_qgemm3(const Geom& g, const float* Sh, const float* G, float* gimg, float* Q, hipStream_t s) {
+void launch_split_g(const Geom& g, const float* G, float* gimg, hipStream_t s) {
   const int total = 4 * (g.H / 16) * (g.H / 32) * 64;
-  bf16x8* gi = reinterpret_cast<bf16x8*>(gimg);
-  k_split_g<<<(total + kThreads - 1) / kThreads, kThreads, 0, s>>>(g.H, G, gi);
+  k_split_g<<<(total + kThreads - 1) / kThreads, kThreads, 0, s>>>(g.H, G, reinterpret_cast<bf16x8*>(gimg));
+}
+
+void launch_qgemm3_img(const Geom& g, const float* Sh, const float* gimg, float* Q, const int* found, hipStream_t s) {
   const int64_t nrt = (g.BT() + Q3_BM - 1) / Q3_BM;
   dim3 grid((unsigned)(nrt * 4 * (g.H / Q3_BN)));
-  k_qgemm3<<<grid, kThreads, 0, s>>>(g, Sh, gi, Q);
+  k_qgemm3<<<grid, kThreads, 0, s>>>(g, Sh, reinterpret_cast<const bf16x8*>(gimg), Q, found);
+}
+
+void launch_qgemm3(const Geom& g, const float* Sh, const float* G, float* gimg, float* Q, hipStream_t s) {
+  launch_split_g(g, G, gimg, s);
+  launch_qgemm3_img(g, Sh, gimg, Q, nullptr, s);
 }
 
 }  // namespace admm

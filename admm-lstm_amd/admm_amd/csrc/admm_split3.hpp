@@ -1,0 +1,117 @@
+// admm_split3.hpp -- split-bf16 MFMA pieces shared by admm_split3.hip (k_qgemm3) and
+// admm_kernels.hip (k_qtrial3, the h-side trial pass fused with Q = Hprev G).  See the header
+// comment of admm_split3.hip for the three-way split and the LDS images.
+#pragma once
+#include "admm_dev.hpp"
+#include "admm_kernels.hpp"
+
+namespace admm {
+namespace {
+
+typedef float f32x8 __attribute__((ext_vector_type(8)));
+
+#ifndef S3_ABL
+#define S3_ABL 0   // kernel ablations for tools/kbench (bitmask, 0 = full kernels)
+#endif
+
+__device__ __forceinline__ int sw_off(int r, int h) {   // bf16 offset of half h of row r
+  return r * 16 + 8 * (h ^ (((r >> 2) ^ (r >> 3)) & 1));
+}
+
+// the six piece products, smallest first: (a2 b0, a1 b1, a0 b2, a1 b0, a0 b1, a0 b0)
+__device__ __forceinline__ f32x16 mfma_split3(const bf16x8 (&a)[3], const bf16x8 (&b)[3], f32x16 acc) {
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[2], b[0], acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], b[1], acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[2], acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], b[0], acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[1], acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[0], acc, 0, 0, 0);
+  return acc;
+}
+
+__device__ __forceinline__ void frag3(const __bf16* img, int piece_stride, int off, bf16x8 (&f)[3]) {
+#pragma unroll
+  for (int p = 0; p < 3; ++p) f[p] = *reinterpret_cast<const bf16x8*>(img + p * piece_stride + off);
+}
+
+__device__ __forceinline__ void put3(__bf16* img, int piece_stride, int off, f32x8 v) {
+  bf16x8 p0, p1, p2;
+  split3(v, p0, p1, p2);
+  *reinterpret_cast<bf16x8*>(img + off) = p0;
+  *reinterpret_cast<bf16x8*>(img + piece_stride + off) = p1;
+  *reinterpret_cast<bf16x8*>(img + 2 * piece_stride + off) = p2;
+}
+
+// ------------------------------------------------------------------ Q tile = Hprev G
+// Tile: 128 rows x 256 columns of one gate (H % 256 == 0), 4 waves as 2 (rows) x 2 (columns)
+// of 64 x 128; K = H in 16-deep steps through double-buffered LDS, the global loads of step
+// c+1 in flight during the MFMAs of step c.  G comes as the split image of k_split_g:
+// gi[(((q * NK + c) * NTT + n) * 3 + p) * 64 + lane] = piece p of the MFMA B fragment of
+// rows 16c.., columns 32n.. (NK = H/16, NTT = H/32).  Ends with a __syncthreads(): the LDS
+// (kQ3Lds bytes from `lds`) is free for the caller's epilogue.
+constexpr int Q3_BM = 128, Q3_BN = 256;
+constexpr int kQ3AP = Q3_BM * 16;               // one piece of the A image (bf16)
+constexpr int kQ3BU = (Q3_BN / 32) * 3 * 64;    // bf16x8 units of one B step image
+constexpr int kQ3Lds = 2 * 3 * kQ3AP * 2 + 2 * kQ3BU * 16;
+
+__device__ __forceinline__ void qgemm3_tile(const Geom& g, const float* __restrict__ Sh,
+                                            const bf16x8* __restrict__ gi, int q, int cb, int64_t m0,
+                                            char* lds, f32x16 (&acc)[2][4]) {
+  constexpr int AP = kQ3AP, BU = kQ3BU;
+  __bf16* As = reinterpret_cast<__bf16*>(lds);                       // [2][3 * AP]
+  bf16x8* Bs = reinterpret_cast<bf16x8*>(lds + 2 * 3 * AP * 2);       // [2][BU]
+  const int H = g.H, NK = H / 16, NTT = H / 32;
+  const int64_t BT = g.BT();
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  // staging: thread = (row sr, k-half sh) of A; 6 units of the B image
+  const int sr = tid >> 1, sh = tid & 1;
+  const int64_t arow = m0 + sr < BT ? m0 + sr : BT - 1;   // rows past BT: computed, not used
+  const float* ap = Sh + g.hrow(arow) * H + 8 * sh;
+  const bf16x8* bp = gi + ((size_t)q * NK * NTT + (size_t)(Q3_BN / 32) * cb) * 192 + tid;
+  const size_t bstep = (size_t)NTT * 192;
+  float4 ra0, ra1;
+  bf16x8 rb[BU / kThreads];
+  auto gload = [&](int c) {
+    if (S3_ABL & 32) {
+      ra0 = make_float4(c, 1.f, 2.f, 3.f); ra1 = ra0;
+    } else {
+      ra0 = *reinterpret_cast<const float4*>(ap + 16 * c);
+      ra1 = *reinterpret_cast<const float4*>(ap + 16 * c + 4);
+    }
+#pragma unroll
+    for (int u = 0; u < BU / kThreads; ++u) rb[u] = bp[c * bstep + u * kThreads];
+  };
+  auto lstore = [&](int st) {
+    put3(As + st * 3 * AP, AP, sw_off(sr, sh), f32x8{ra0.x, ra0.y, ra0.z, ra0.w, ra1.x, ra1.y, ra1.z, ra1.w});
+#pragma unroll
+    for (int u = 0; u < BU / kThreads; ++u) Bs[st * BU + tid + u * kThreads] = rb[u];
+  };
+  const int wr = wave >> 1, wc = wave & 1, c32 = lane & 31, kh = lane >> 5;
+  zero_acc(acc);
+  gload(0);
+  lstore(0);
+  __syncthreads();
+  for (int c = 0; c < NK; ++c) {
+    const int st = c & 1;
+    if (c + 1 < NK) gload(c + 1);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int mi = 0; mi < 2; ++mi) {
+      bf16x8 a[3];
+      frag3(As + st * 3 * AP, AP, sw_off(wr * 64 + mi * 32 + c32, kh), a);
+#pragma unroll
+      for (int ni = 0; ni < 4; ++ni) {
+        const bf16x8* bb = &Bs[st * BU + (wc * 4 + ni) * 192 + lane];
+        const bf16x8 b[3] = {bb[0], bb[64], bb[128]};
+        if (S3_ABL & 64) acc[mi][ni][0] += (float)a[0][0] * (float)b[0][0];
+        else acc[mi][ni] = mfma_split3(a, b, acc[mi][ni]);
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    if (c + 1 < NK) lstore(st ^ 1);
+    __syncthreads();
+  }
+}
+
+}  // namespace
+}  // namespace admm

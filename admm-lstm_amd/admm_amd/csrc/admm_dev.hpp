@@ -203,11 +203,16 @@ __device__ __forceinline__ void buf_st4(__amdgpu_buffer_rsrc_t r, uint32_t off, 
   __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned int, v), r,
                                          (int)off, 0, AUX);
 }
-// store at voffset + soffset (soffset wave-uniform: one descriptor serves several planes)
+// store at off + soff (one descriptor serving several planes).  The plane offset goes into the
+// VGPR offset, never the SGPR soffset field: LLVM assumes a >64-bit MUBUF store that names an
+// soffset register has no store-data hazard and lets the next VALU overwrite the data VGPRs
+// immediately, but on gfx950 such stores wrote clobbered data (the first ones of a back-to-back
+// group, lane-dependent; DESIGN.md, "tgt from the sweep").  With soffset 0 the compiler inserts
+// the wait states.
 template <int AUX = 2>
 __device__ __forceinline__ void buf_st4s(__amdgpu_buffer_rsrc_t r, uint32_t off, uint32_t soff, f32x4 v) {
   __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned int, v), r,
-                                         (int)off, (int)soff, AUX);
+                                         (int)(off + soff), 0, AUX);
 }
 template <int AUX = 2>
 __device__ __forceinline__ void buf_st(__amdgpu_buffer_rsrc_t r, uint32_t off, float v) {

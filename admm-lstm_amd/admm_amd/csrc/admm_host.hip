@@ -68,10 +68,9 @@ struct AdmmCtx {
   bool z_valid = false;
   bool force_generic = false;  // weight stages on the generic kernels (ADMM_GENERIC=1; tests)
   bool tgt_valid = false;  // tgt holds lam/rho + S of the current state (left by the persistent sweep)
-  // let the persistent sweep write tgt for the next x stage (ADMM_TGT_SWEEP=1).  Off: with it on,
-  // C2 trajectories turn non-finite at a random step (x stage of gate g) although z and tgt
-  // are finite and tgt equals lam/rho + S when checked on device; not yet understood
-  bool tgt_sweep = false;
+  // the persistent sweep writes tgt for the next x stage, which then reads it instead of
+  // recomputing it from the gate and dual planes (ADMM_TGT_SWEEP=0 disables)
+  bool tgt_sweep = true;
   int steps = 0;
   // workspace (all device)
   float *zc = nullptr, *tgt = nullptr, *R = nullptr, *Q = nullptr;  // [4][BT][H]

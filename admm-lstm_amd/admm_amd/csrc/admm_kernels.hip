@@ -136,6 +136,11 @@ __global__ __launch_bounds__(kThreads) void k_forward_t(Geom g, int t, Weights w
   }
 }
 
+// The line-search target tgt = lam / rho + S of a gate (the lam/rho + S term of the residual,
+// admm.py:302-312), written by k_resid_gx or by the persistent sweep: one expression (IEEE
+// division, as the reference) so that either source gives equal bits.
+__device__ __forceinline__ f32x4 tgt_quot(f32x4 lam, float rho, f32x4 s) { return lam / rho + s; }
+
 // ---- one (b, j) point of the time sweep: i, f, g, o (admm.py:353-386), c (388-436),
 // h for t < T (455-457), duals of i, f, g, o, c (504-530).  Operand grouping follows the
 // reference expression by expression (fp32).
@@ -494,9 +499,9 @@ __global__ __launch_bounds__(SR_THREADS) void k_sweep_rows(Geom g, const bf16x8*
         buf_st4s(rZ, zo4, 0, zi); buf_st4s(rZ, zo4, zpl, zf); buf_st4s(rZ, zo4, 2 * zpl, zg);
         buf_st4s(rZ, zo4, 3 * zpl, zo);
       }
-      if (wtgt && rok) {   // same expression as k_resid_gx (IEEE division), so either source gives equal bits
-        buf_st4s(rT, zo4, 0, li / hp.rho[0] + i1); buf_st4s(rT, zo4, zpl, lf / hp.rho[1] + f1);
-        buf_st4s(rT, zo4, 2 * zpl, lg / hp.rho[2] + g1); buf_st4s(rT, zo4, 3 * zpl, lo / hp.rho[3] + o1);
+      if (wtgt && rok) {   // same expression as k_resid_gx (tgt_quot), so either source gives equal bits
+        buf_st4s(rT, zo4, 0, tgt_quot(li, hp.rho[0], i1)); buf_st4s(rT, zo4, zpl, tgt_quot(lf, hp.rho[1], f1));
+        buf_st4s(rT, zo4, 2 * zpl, tgt_quot(lg, hp.rho[2], g1)); buf_st4s(rT, zo4, 3 * zpl, tgt_quot(lo, hp.rho[3], o1));
       }
 #ifdef SR_TIMING
       const unsigned long long tc_ = clock64();
@@ -1504,7 +1509,8 @@ __global__ __launch_bounds__(kThreads) void k_resid_gx(Geom g, Hyper hp, const f
       } else {
         const float4 l4 = ld_nt(Lq + so + j);
         const float4 s4 = ld_nt(Sq + so + j);
-        t4.x = l4.x / rho + s4.x; t4.y = l4.y / rho + s4.y; t4.z = l4.z / rho + s4.z; t4.w = l4.w / rho + s4.w;
+        const f32x4 tv = tgt_quot(f32x4{l4.x, l4.y, l4.z, l4.w}, rho, f32x4{s4.x, s4.y, s4.z, s4.w});
+        t4 = make_float4(tv.x, tv.y, tv.z, tv.w);
         st_nt(tq + row * g.H + j, t4);
       }
       const float zz[4] = {z4.x, z4.y, z4.z, z4.w}, tt[4] = {t4.x, t4.y, t4.z, t4.w};

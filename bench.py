@@ -64,12 +64,19 @@ def make_data(gen: str, B: int, T: int, D: int, seed_offset: int = 0):
     return s[idx].unsqueeze(2).contiguous(), s[torch.arange(B) + T].unsqueeze(1).contiguous()
 
 
+def tgt_from_sweep(H: int) -> bool:
+    """The persistent sweep (64 <= H <= 256) writes the next x stage's targets unless disabled."""
+    return 64 <= H <= 256 and os.environ.get('ADMM_TGT_SWEEP', '1') != '0'
+
+
 def roofline_terms(cls: str, B: int, T: int, D: int, H: int):
     """Algorithmic (flops, bytes) of ONE launch of a kernel class."""
     f4 = 4  # bytes per fp32
+    tgt = tgt_from_sweep(H)
     if cls == 'sweep':            # whole sweep t = 1..T: per t [B, D+H] x [D+H, 4H] + fused gate/dual updates
-        # per (b, t, j): 11 state/dual loads (incl. c_{t-1}), 15 stores (6 gates, 5 duals, 4 z)
-        return T * 2.0 * B * (D + H) * 4 * H, T * f4 * B * (D + 26 * H)
+        # per (b, t, j): 11 state/dual loads (incl. c_{t-1}), 15 stores (6 gates, 5 duals, 4 z),
+        # + 4 tgt stores when the sweep writes the next x stage's targets
+        return T * 2.0 * B * (D + H) * 4 * H, T * f4 * B * (D + (30 if tgt else 26) * H)
     n = float(B) * T * H          # elements of one [B*T, H] plane
     if cls == 'atr_h':            # G_q = Hprev^T R_q, 4 gates
         return 2.0 * B * T * H * 4 * H, f4 * (B * T * H + 4 * n)
@@ -81,8 +88,8 @@ def roofline_terms(cls: str, B: int, T: int, D: int, H: int):
         return 2.0 * B * T * D * 4 * H, f4 * (B * T * D + 4 * n)
     if cls in ('trial', 'trial_extra'):  # read z, tgt, Q per element
         return 0.0, f4 * 3 * 4 * n
-    if cls == 'resid':            # read z, lam, S (or z, tgt, x); write tgt/z, R
-        return 0.0, f4 * 5 * 4 * n
+    if cls == 'resid':            # x-stage residual (read z and tgt, or z, lam, S and write tgt) + z += X dWx
+        return 0.0, f4 * ((2 if tgt else 4) + 2) * 4 * n
     return None
 
 

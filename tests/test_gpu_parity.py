@@ -531,3 +531,34 @@ def test_z_cache_matches_recompute(shape, mods, dev):
         ref = X @ wx + hp @ wh
         scale = (X.abs() @ wx.abs() + hp.abs() @ wh.abs()).max().item()
         assert float((buf[qi].double() - ref).abs().max()) <= 1e-5 * scale, q
+
+
+@pytest.mark.parametrize('shape', [(300, 3, 16, 64), (2048, 4, 16, 64), (300, 3, 16, 256)])
+def test_tgt_from_sweep_bit_identical(shape, mods, dev, monkeypatch):
+    """The persistent sweep writes tgt = lam/rho + S for the next x stage (default), which then
+    skips reading the gate and dual planes; with ADMM_TGT_SWEEP=0 the x stage recomputes it.  Both
+    must give bit-identical trajectories (same expression, same inputs).  Covers the gfx950 store
+    hazard of buf_st4s (plane offsets in the SGPR soffset field clobbered the stored tgt) and a
+    ragged last row block (B % 32 != 0)."""
+    from blocks.lstm import LSTM
+    from parameters import example_parameter_dictionary
+    admm, _ = mods
+    admm.with_dual_y = False
+    B, T, D, H = shape
+    g = torch.Generator().manual_seed(11)
+    x = torch.rand(B, T, D, generator=g).to(dev)
+    y = torch.rand(B, 1, generator=g).to(dev)
+    out = []
+    for mode in ('0', '1'):
+        monkeypatch.setenv('ADMM_TGT_SWEEP', mode)
+        torch.manual_seed(0)
+        m = LSTM(D, H, 1).to(dev)
+        opt = admm.ADMMBasedOptimizer(m, (x, y), example_parameter_dictionary['GoogleStock'], verbose=False)
+        for _ in range(3):
+            opt.step()
+        out.append((torch.cat([p.detach().flatten() for p in m.parameters()]),
+                    torch.cat([v.flatten() for v in opt.gates.values()] + [v.flatten() for v in opt.duals.values()])))
+        del opt
+    assert torch.isfinite(out[1][0]).all() and torch.isfinite(out[1][1]).all()
+    assert torch.equal(out[0][0], out[1][0])
+    assert torch.equal(out[0][1], out[1][1])

@@ -95,7 +95,7 @@ def roofline_terms(cls: str, B: int, T: int, D: int, H: int):
 
 # kernel symbols of each profile class (admm_kernels.hip), for the committed PMC traffic
 CLASS_KERNELS = {'sweep': ('k_sweep_rows', 'k_sweep_t'), 'atr_h': ('k_atr3', 'k_atr_fused', 'k_atr<128'), 'qgemm_h': ('k_qgemm3', 'k_qgemm<true, 1>'),
-                 'trial': ('k_trial_rows', 'k_qtrial3', 'k_trial_fast', 'k_trial<'), 'resid': ('k_resid_gx', 'k_apply_dwx', 'k_resid<')}
+                 'trial': ('k_trial_rows', 'k_trial_fast', 'k_trial<'), 'resid': ('k_resid_gx', 'k_apply_dwx', 'k_resid<')}
 
 
 def pmc_traffic(cls: str, cfg_name: str):

@@ -818,8 +818,19 @@ __global__ __launch_bounds__(kThreads) void k_reduce_g(int Kd, int H, Hyper hp, 
   if (i < 4) found[i] = 0;   // this stage's line searches start undecided (no memset launch)
   if (i >= 4 * per_q) return;
   const int q = (int)(i / per_q);
+  // sequential fp64 sum over the splits (fixed order: deterministic), loads issued 8 at a time
+  const float* p = slab + i;
+  const int64_t st = 4 * per_q;
   double s = 0.0;
-  for (int sp = 0; sp < nsplit; ++sp) s += (double)slab[(int64_t)sp * 4 * per_q + i];
+  int sp = 0;
+  for (; sp + 8 <= nsplit; sp += 8) {
+    float v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = p[(int64_t)(sp + u) * st];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) s += (double)v[u];
+  }
+  for (; sp < nsplit; ++sp) s += (double)p[(int64_t)sp * st];
   G[i] = (float)s * hp.rho[q];  // (sum_t A_t^T R_t) * rho (admm.py:312)
 }
 
@@ -1719,8 +1730,19 @@ __global__ __launch_bounds__(kThreads) void k_wy_slab(Geom g, const float* Sh, c
   const int64_t per = (g.B + nsplit - 1) / nsplit;
   const int64_t b0 = blockIdx.y * per, b1 = (b0 + per < g.B) ? b0 + per : g.B;
   const int64_t rs = (int64_t)g.TP() * g.H;
+  // sequential sum over the rows (fixed order), the h_T and U loads issued 8 rows at a time
+  const float* hp = Sh + (int64_t)g.T * g.H + j;
+  const float* up = U + o;
   float s = 0.f;
-  for (int64_t b = b0; b < b1; ++b) s += Sh[b * rs + (int64_t)g.T * g.H + j] * U[b * g.O + o];
+  int64_t b = b0;
+  for (; b + 8 <= b1; b += 8) {
+    float hv[8], uv[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) { hv[u] = hp[(b + u) * rs]; uv[u] = up[(b + u) * g.O]; }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) s += hv[u] * uv[u];
+  }
+  for (; b < b1; ++b) s += hp[b * rs] * up[b * g.O];
   slab[blockIdx.y * nHO + i] = s;
 }
 

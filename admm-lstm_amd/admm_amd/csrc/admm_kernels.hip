@@ -1527,9 +1527,18 @@ __global__ __launch_bounds__(kThreads) void k_resid_gx(Geom g, Hyper hp, const f
       const float zz[4] = {z4.x, z4.y, z4.z, z4.w}, tt[4] = {t4.x, t4.y, t4.z, t4.w};
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
+        // the activation of the stored gates (sig_pair / tanhf, as k_forward_t and k_resid): at
+        // step 1 S = phi(z) bit for bit, so R and G_x are exactly zero as in the reference
+        // (admm.py:302-312) and the x-side searches take k = 0, not a decision on rounding noise
         float phi, dphi;
-        if (th) phi_fast<true>(zz[u], phi, dphi);
-        else phi_fast<false>(zz[u], phi, dphi);
+        if (th) {
+          phi = tanhf(zz[u]);
+          dphi = 1.f - phi * phi;
+        } else {
+          const SigPair sp = sig_pair(zz[u]);
+          phi = sp.s;
+          dphi = sp.s * sp.sc;
+        }
         const float R = (phi - tt[u]) * dphi;
 #pragma unroll
         for (int d = 0; d < DP; ++d) acc[d][u] += xr[d] * R;

@@ -1780,16 +1780,21 @@ __global__ __launch_bounds__(kThreads) void k_wy_apply(int64_t nHO, Hyper hp, co
 // gamma = rho_h), candidates beta(theta) for theta = 0.1 * 2^c.
 constexpr int kMaxO = 8;
 
-struct HTRow {
-  float u[kMaxO];
+template <int N>
+struct HTRowT {
+  float u[N];
 };
+// array width for a compile-time output count (O = 1: registers), else the runtime bound kMaxO
+#define HT_W (OC > 0 ? OC : kMaxO)
 
+template <int OC>
 __device__ __forceinline__ void ht_row_u(const Geom& g, const float* h, const float* a_row, const float* s_row,
-                                         const float* wy, HTRow& r) {
+                                         const float* wy, HTRowT<HT_W>& r) {
+  const int NO = OC > 0 ? OC : g.O;   // output width: compile-time for O = 1 (arrays stay in registers)
   const int lane = threadIdx.x & 63;
-  for (int o = 0; o < g.O; ++o) {
+  for (int o = 0; o < NO; ++o) {
     float s = 0.f;
-    for (int j = lane; j < g.H; j += kWave) s += h[j] * wy[(int64_t)j * g.O + o];
+    for (int j = lane; j < g.H; j += kWave) s += h[j] * wy[(int64_t)j * NO + o];
     s = wave_sum(s);
     float u = s - a_row[o];
     if (s_row) u = u - s_row[o];
@@ -1797,19 +1802,23 @@ __device__ __forceinline__ void ht_row_u(const Geom& g, const float* h, const fl
   }
 }
 
-__device__ __forceinline__ float ht_grad(const Geom& g, const Hyper& hp, const HTRow& r, const float* wy, int j) {
+template <int OC>
+__device__ __forceinline__ float ht_grad(const Geom& g, const Hyper& hp, const HTRowT<HT_W>& r, const float* wy, int j) {
+  const int NO = OC > 0 ? OC : g.O;   // output width: compile-time for O = 1 (arrays stay in registers)
   float s = 0.f;
   if (hp.variant == 0) {
     const float ry = hp.rho[6];
-    for (int o = 0; o < g.O; ++o) s += (ry * r.u[o]) * wy[(int64_t)j * g.O + o];
+    for (int o = 0; o < NO; ++o) s += (ry * r.u[o]) * wy[(int64_t)j * NO + o];
     return s;
   }
-  for (int o = 0; o < g.O; ++o) s += r.u[o] * wy[(int64_t)j * g.O + o];
+  for (int o = 0; o < NO; ++o) s += r.u[o] * wy[(int64_t)j * NO + o];
   return hp.rho[5] * s;
 }
 
+template <int OC>
 __global__ __launch_bounds__(kThreads) void k_ht_partial(Geom g, Hyper hp, Planes6 S, Planes6 L, const float* a,
                                                            const float* Ly, const float* wy, double* part) {
+  const int NO = OC > 0 ? OC : g.O;   // output width: compile-time for O = 1 (arrays stay in registers)
   __shared__ double red[4];
   __shared__ double accs[4][kHTSums];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -1819,25 +1828,25 @@ __global__ __launch_bounds__(kThreads) void k_ht_partial(Geom g, Hyper hp, Plane
   const int64_t rs = (int64_t)g.TP() * g.H, tofs = (int64_t)g.T * g.H;
   double acc[kHTSums];
   for (int i = 0; i < kHTSums; ++i) acc[i] = 0.0;
-  float sbuf[kMaxO];
+  float sbuf[HT_W];
   for (int64_t b = (int64_t)blockIdx.x * 4 + w; b < g.B; b += (int64_t)gridDim.x * 4) {
     const float* h = S.p[5] + b * rs + tofs;
     const float* o_ = S.p[3] + b * rs + tofs;
     const float* c_ = S.p[4] + b * rs + tofs;
     const float* lh = L.p[5] + b * rs + tofs;
     if (shift)
-      for (int o = 0; o < g.O; ++o) sbuf[o] = Ly[b * g.O + o] / ry;
-    HTRow r;
-    ht_row_u(g, h, a + b * g.O, shift ? sbuf : nullptr, wy, r);
+      for (int o = 0; o < NO; ++o) sbuf[o] = Ly[b * NO + o] / ry;
+    HTRowT<HT_W> r;
+    ht_row_u<OC>(g, h, a + b * NO, shift ? sbuf : nullptr, wy, r);
     float fh = 0.f;
-    for (int o = 0; o < g.O; ++o) fh += r.u[o] * r.u[o];
-    float v[kHTCand][kMaxO], ip[kHTCand], nq[kHTCand];
+    for (int o = 0; o < NO; ++o) fh += r.u[o] * r.u[o];
+    float v[kHTCand][HT_W], ip[kHTCand], nq[kHTCand];
     for (int c = 0; c < kHTCand; ++c) {
       ip[c] = 0.f; nq[c] = 0.f;
-      for (int o = 0; o < g.O; ++o) v[c][o] = 0.f;
+      for (int o = 0; o < NO; ++o) v[c][o] = 0.f;
     }
     for (int j = lane; j < g.H; j += kWave) {
-      const float gj = ht_grad(g, hp, r, wy, j);
+      const float gj = ht_grad<OC>(g, hp, r, wy, j);
       const float hj = h[j], pj = rh * o_[j] * tanhf(c_[j]) - lh[j];
       for (int c = 0; c < kHTCand; ++c) {
         const float th = ldexpf(0.1f, c);
@@ -1845,15 +1854,15 @@ __global__ __launch_bounds__(kThreads) void k_ht_partial(Geom g, Hyper hp, Plane
         const float dj = bj - hj;
         ip[c] += gj * dj;
         nq[c] += dj * dj;
-        for (int o = 0; o < g.O; ++o) v[c][o] += bj * wy[(int64_t)j * g.O + o];
+        for (int o = 0; o < NO; ++o) v[c][o] += bj * wy[(int64_t)j * NO + o];
       }
     }
     // wave-reduce and accumulate (lane 0 holds the row's values)
     acc[0] += (double)fh;  // identical on every lane
     for (int c = 0; c < kHTCand; ++c) {
       float fb = 0.f;
-      for (int o = 0; o < g.O; ++o) {
-        float vv = wave_sum(v[c][o]) - a[b * g.O + o];
+      for (int o = 0; o < NO; ++o) {
+        float vv = wave_sum(v[c][o]) - a[b * NO + o];
         if (shift) vv = vv - sbuf[o];
         fb += vv * vv;
       }
@@ -1898,9 +1907,11 @@ __device__ __forceinline__ float ht_theta_star(const Hyper& hp, const double* su
 
 // h_T update with theta* (admm.py:482-487), a update (489-502), dual h at T (532-539),
 // dual y (541-546, admm variant with with_dual_y).
+template <int OC>
 __global__ __launch_bounds__(kThreads) void k_ht_apply(Geom g, Hyper hp, Planes6 S, Planes6 L, float* a, float* Ly,
                                                          const float* y, const float* wy, const double* sums,
                                                          DevStats* stats) {
+  const int NO = OC > 0 ? OC : g.O;   // output width: compile-time for O = 1 (arrays stay in registers)
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const float ry = hp.rho[6], rh = hp.rho[5];
   const bool nd = hp.variant == 1;
@@ -1909,30 +1920,30 @@ __global__ __launch_bounds__(kThreads) void k_ht_apply(Geom g, Hyper hp, Planes6
   if (blockIdx.x == 0 && threadIdx.x == 0) stats->theta_h = th;
   const int64_t rs = (int64_t)g.TP() * g.H, tofs = (int64_t)g.T * g.H;
   const float Bry = (float)g.Bg * ry;
-  float sbuf[kMaxO];
+  float sbuf[HT_W];
   for (int64_t b = (int64_t)blockIdx.x * 4 + w; b < g.B; b += (int64_t)gridDim.x * 4) {
     float* h = S.p[5] + b * rs + tofs;
     const float* o_ = S.p[3] + b * rs + tofs;
     const float* c_ = S.p[4] + b * rs + tofs;
     float* lh = L.p[5] + b * rs + tofs;
     if (shift)
-      for (int o = 0; o < g.O; ++o) sbuf[o] = Ly[b * g.O + o] / ry;
-    HTRow r;
-    ht_row_u(g, h, a + b * g.O, shift ? sbuf : nullptr, wy, r);
-    float hw[kMaxO];
-    for (int o = 0; o < g.O; ++o) hw[o] = 0.f;
+      for (int o = 0; o < NO; ++o) sbuf[o] = Ly[b * NO + o] / ry;
+    HTRowT<HT_W> r;
+    ht_row_u<OC>(g, h, a + b * NO, shift ? sbuf : nullptr, wy, r);
+    float hw[HT_W];
+    for (int o = 0; o < NO; ++o) hw[o] = 0.f;
     for (int j = lane; j < g.H; j += kWave) {
-      const float gj = ht_grad(g, hp, r, wy, j);
+      const float gj = ht_grad<OC>(g, hp, r, wy, j);
       const float tc = tanhf(c_[j]);
       const float hn = (th * h[j] + rh * o_[j] * tc - lh[j] - gj) / (th + rh);
       h[j] = hn;
       lh[j] = lh[j] + rh * (hn - o_[j] * tc);
-      for (int o = 0; o < g.O; ++o) hw[o] += hn * wy[(int64_t)j * g.O + o];
+      for (int o = 0; o < NO; ++o) hw[o] += hn * wy[(int64_t)j * NO + o];
     }
-    for (int o = 0; o < g.O; ++o) {
+    for (int o = 0; o < NO; ++o) {
       const float hwo = wave_sum(hw[o]);
       if (lane == 0) {
-        const int64_t i = b * g.O + o;
+        const int64_t i = b * NO + o;
         float an;
         if (!nd) {
           const float corr = shift ? (float)g.Bg * Ly[i] : 0.f;
@@ -2217,7 +2228,8 @@ int ht_blocks(const Geom& g) {
 
 void launch_ht_partial(const Geom& g, const Hyper& hp, const Planes6& S, const Planes6& L, const float* a,
                        const float* Ly, const float* wy, double* part, int nblk, hipStream_t s) {
-  k_ht_partial<<<nblk, kThreads, 0, s>>>(g, hp, S, L, a, Ly, wy, part);
+  if (g.O == 1) k_ht_partial<1><<<nblk, kThreads, 0, s>>>(g, hp, S, L, a, Ly, wy, part);
+  else k_ht_partial<0><<<nblk, kThreads, 0, s>>>(g, hp, S, L, a, Ly, wy, part);
 }
 
 void launch_ht_reduce(const double* part, int nblk, double* sums, hipStream_t s) {
@@ -2226,7 +2238,8 @@ void launch_ht_reduce(const double* part, int nblk, double* sums, hipStream_t s)
 
 void launch_ht_apply(const Geom& g, const Hyper& hp, const Planes6& S, const Planes6& L, float* a, float* Ly,
                      const float* y, const float* wy, const double* sums, DevStats* stats, hipStream_t s) {
-  k_ht_apply<<<ht_blocks(g), kThreads, 0, s>>>(g, hp, S, L, a, Ly, y, wy, sums, stats);
+  if (g.O == 1) k_ht_apply<1><<<ht_blocks(g), kThreads, 0, s>>>(g, hp, S, L, a, Ly, y, wy, sums, stats);
+  else k_ht_apply<0><<<ht_blocks(g), kThreads, 0, s>>>(g, hp, S, L, a, Ly, y, wy, sums, stats);
 }
 
 }  // namespace admm

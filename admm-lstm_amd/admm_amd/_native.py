@@ -73,7 +73,9 @@ _SIGNATURES = {
     'admm_invalidate_cache': (c_int, [c_void_p]),
     'admm_comm_unique_id': (c_int, [c_void_p, c_int64]),
     'admm_set_comm': (c_int, [c_void_p, c_void_p, c_int64, c_int, c_int]),
+    'admm_set_comm_host': (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int]),
     'admm_get_stats': (c_int, [c_void_p, POINTER(AdmmStats)]),
+    'admm_poll_status': (c_int, [c_void_p, POINTER(c_int32), POINTER(c_int32)]),
     'admm_profile': (c_int, [c_void_p, ctypes.c_uint32]),
     'admm_profile_read': (c_int, [c_void_p, POINTER(c_double), POINTER(c_int32)]),
     'admm_debug_workspace': (c_int, [c_void_p, c_int32, c_void_p, c_int64, c_void_p]),
@@ -83,6 +85,9 @@ _SIGNATURES = {
                              c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
 }
 EXPORTS = tuple(_SIGNATURES)
+
+# int (*admm_host_allreduce_fn)(void* host_buf, int64_t count, int32_t dtype, void* user)
+HOST_ALLREDUCE_FN = ctypes.CFUNCTYPE(c_int, c_void_p, c_int64, c_int32, c_void_p)
 
 _lib = None
 

@@ -46,6 +46,25 @@ int fail(int code, const char* fmt, ...) {
     if (r_ != ncclSuccess) return fail(ADMM_ECOMM, "%s failed: %s", #expr, ncclGetErrorString(r_)); \
   } while (0)
 
+// Sets the context's device for the duration of one C-ABI call and restores the caller's
+// current device on return, so torch's current device is not moved by the library.
+struct DeviceGuard {
+  int prev = -1;
+  hipError_t err;
+  explicit DeviceGuard(int dev) {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    err = prev == dev ? hipSuccess : hipSetDevice(dev);
+  }
+  ~DeviceGuard() {
+    int cur = -1;
+    if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+  }
+};
+
+#define DEVICE_GUARD(dev)                                                                          \
+  DeviceGuard dg_(dev);                                                                            \
+  if (dg_.err != hipSuccess) return fail(ADMM_EHIP, "hipSetDevice(%d) failed: %s", (int)(dev), hipGetErrorString(dg_.err))
+
 template <typename T>
 int dalloc(T** p, size_t n) {
   *p = nullptr;
@@ -94,6 +113,14 @@ struct AdmmCtx {
   // multi-GPU
   ncclComm_t comm = nullptr;
   int rank = 0, world = 1;
+  // host-staged communicator (admm_set_comm_host): stream sync + D2H + callback + H2D
+  admm_host_allreduce_fn host_ar = nullptr;
+  void* host_ar_user = nullptr;
+  std::vector<double> host_stage;
+  // host-mapped mirror of DevStats {unresolved, nonfinite}, written by the step's last
+  // kernel and read without a sync by admm_poll_status
+  int* status_host = nullptr;
+  int* status_dev = nullptr;
   // optional live kernel timing (admm_profile): hipEvent pairs around launches of the
   // selected kernel classes, on the launch stream
   uint32_t prof_mask = 0;
@@ -150,7 +177,22 @@ Planes6 planes(float* const p[6]) {
   return r;
 }
 
+// Host-staged all-reduce (admm_set_comm_host): a test / fallback path, not the RCCL one.
+int allreduce_host(AdmmCtx* c, void* p, size_t n, int dtype, hipStream_t s) {
+  const size_t bytes = n * (dtype == 0 ? sizeof(float) : sizeof(double));
+  if (c->host_stage.size() * sizeof(double) < bytes) c->host_stage.resize((bytes + 7) / 8);
+  void* h = c->host_stage.data();
+  HIP_TRY(hipMemcpyAsync(h, p, bytes, hipMemcpyDeviceToHost, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  const int rc = c->host_ar(h, (int64_t)n, dtype, c->host_ar_user);
+  if (rc != 0) return fail(ADMM_ECOMM, "host all-reduce callback returned %d", rc);
+  HIP_TRY(hipMemcpyAsync(p, h, bytes, hipMemcpyHostToDevice, s));
+  HIP_TRY(hipStreamSynchronize(s));
+  return ADMM_OK;
+}
+
 int allreduce_f32(AdmmCtx* c, float* p, size_t n, hipStream_t s) {
+  if (c->host_ar) return allreduce_host(c, p, n, 0, s);
   if (!c->comm) return ADMM_OK;
   ProfScope ps(c, ADMM_PROF_COMM, s);
   NCCL_TRY(ncclAllReduce(p, p, n, ncclFloat32, ncclSum, c->comm, s));
@@ -158,6 +200,7 @@ int allreduce_f32(AdmmCtx* c, float* p, size_t n, hipStream_t s) {
 }
 
 int allreduce_f64(AdmmCtx* c, double* p, size_t n, hipStream_t s) {
+  if (c->host_ar) return allreduce_host(c, p, n, 1, s);
   if (!c->comm) return ADMM_OK;
   ProfScope ps(c, ADMM_PROF_COMM, s);
   NCCL_TRY(ncclAllReduce(p, p, n, ncclFloat64, ncclSum, c->comm, s));
@@ -311,7 +354,8 @@ int stage_sweep(AdmmCtx* c, hipStream_t s) {
   launch_ht_reduce(c->ht_part, c->ht_nblk, c->ht_sums, s);
   int rc = allreduce_f64(c, c->ht_sums, kHTSums, s);
   if (rc) return rc;
-  launch_ht_apply(g, c->hp, sa.S, sa.L, c->buf.a, c->buf.dual_y, c->buf.y, c->buf.wy, c->ht_sums, c->stats, s);
+  launch_ht_apply(g, c->hp, sa.S, sa.L, c->buf.a, c->buf.dual_y, c->buf.y, c->buf.wy, c->ht_sums, c->stats,
+                  c->status_dev, s);
   return ADMM_OK;
 }
 
@@ -349,7 +393,7 @@ int admm_create(const AdmmDims* dims, const AdmmParams* params, int device, Admm
     return fail(ADMM_EINVAL, "unknown variant %d", params->variant);
   for (int i = 0; i < 7; ++i)
     if (!std::isfinite(params->rho[i])) return fail(ADMM_EINVAL, "rho[%d] is not finite", i);
-  HIP_TRY(hipSetDevice(device));
+  DEVICE_GUARD(device);
   AdmmCtx* c = new AdmmCtx();
   c->device = device;
   Geom& g = c->g;
@@ -417,18 +461,25 @@ int admm_create(const AdmmDims* dims, const AdmmParams* params, int device, Admm
     admm_destroy(c);
     return fail(ADMM_EHIP, "hipMemset(stats) failed");
   }
+  if (hipHostMalloc((void**)&c->status_host, 2 * sizeof(int), hipHostMallocMapped) != hipSuccess ||
+      hipHostGetDevicePointer((void**)&c->status_dev, c->status_host, 0) != hipSuccess) {
+    admm_destroy(c);
+    return fail(ADMM_EHIP, "mapped status mirror allocation failed");
+  }
+  c->status_host[0] = c->status_host[1] = 0;
   *out = c;
   return ADMM_OK;
 }
 
 int admm_destroy(AdmmCtx* c) {
   if (!c) return ADMM_OK;
-  (void)hipSetDevice(c->device);
+  DeviceGuard dg_(c->device);
   void* ptrs[] = {c->zc, c->tgt, c->R, c->Q, c->G, c->dW, c->gslab, c->tr_part, c->tr_sums, c->tr_poly, c->found, c->pick,
                   c->U, c->wy_slab, c->Gy, c->ht_part, c->ht_sums, c->stats, c->swt, c->gimg};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   if (c->comm) ncclCommDestroy(c->comm);
+  if (c->status_host) (void)hipHostFree(c->status_host);
   for (hipEvent_t e : c->ev_pool) (void)hipEventDestroy(e);
   if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
   for (int p = 0; p < kMaxSweepStreams - 1; ++p) {
@@ -477,7 +528,7 @@ int admm_init_state(AdmmCtx* c, void* stream) {
   if (!c->bound) return fail(ADMM_ESTATE, "admm_init_state before admm_bind");
   hipStream_t s = (hipStream_t)stream;
   const Geom& g = c->g;
-  HIP_TRY(hipSetDevice(c->device));
+  DEVICE_GUARD(c->device);
   const size_t pbytes = (size_t)g.B * g.TP() * g.H * sizeof(float);
   for (int q = 0; q < 6; ++q) {
     HIP_TRY(hipMemsetAsync(c->buf.gates[q], 0, pbytes, s));
@@ -513,7 +564,7 @@ int admm_step(AdmmCtx* c, void* stream) {
   if (!c) return fail(ADMM_EINVAL, "NULL ctx");
   if (!c->bound) return fail(ADMM_ESTATE, "admm_step before admm_bind");
   hipStream_t s = (hipStream_t)stream;
-  HIP_TRY(hipSetDevice(c->device));
+  DEVICE_GUARD(c->device);
   int rc;
   if (!c->z_valid) {
     ProfScope ps(c, ADMM_PROF_ZGEMM, s);
@@ -541,16 +592,40 @@ int admm_comm_unique_id(void* out, int64_t out_bytes) {
 int admm_set_comm(AdmmCtx* c, const void* uid, int64_t id_bytes, int rank, int world) {
   if (!c || !uid || id_bytes < (int64_t)sizeof(ncclUniqueId)) return fail(ADMM_EINVAL, "bad arguments");
   if (world < 1 || rank < 0 || rank >= world) return fail(ADMM_EINVAL, "bad rank %d / world %d", rank, world);
-  HIP_TRY(hipSetDevice(c->device));
+  DEVICE_GUARD(c->device);
   if (c->comm) {
     ncclCommDestroy(c->comm);
     c->comm = nullptr;
   }
+  c->host_ar = nullptr;
   c->rank = rank;
   c->world = world;
   ncclUniqueId id;
   std::memcpy(&id, uid, sizeof id);
   NCCL_TRY(ncclCommInitRank(&c->comm, world, id, rank));
+  return ADMM_OK;
+}
+
+int admm_set_comm_host(AdmmCtx* c, admm_host_allreduce_fn fn, void* user, int rank, int world) {
+  if (!c || !fn) return fail(ADMM_EINVAL, "admm_set_comm_host: NULL argument");
+  if (world < 1 || rank < 0 || rank >= world) return fail(ADMM_EINVAL, "bad rank %d / world %d", rank, world);
+  DEVICE_GUARD(c->device);
+  if (c->comm) {
+    ncclCommDestroy(c->comm);
+    c->comm = nullptr;
+  }
+  c->host_ar = fn;
+  c->host_ar_user = user;
+  c->rank = rank;
+  c->world = world;
+  return ADMM_OK;
+}
+
+int admm_poll_status(AdmmCtx* c, int32_t* unresolved, int32_t* nonfinite) {
+  if (!c || !unresolved || !nonfinite) return fail(ADMM_EINVAL, "admm_poll_status: NULL argument");
+  const volatile int* m = c->status_host;
+  *unresolved = m[0];
+  *nonfinite = m[1];
   return ADMM_OK;
 }
 
@@ -562,7 +637,7 @@ int admm_profile(AdmmCtx* c, uint32_t class_mask) {
 
 int admm_profile_read(AdmmCtx* c, double* ms, int32_t* count) {
   if (!c || !ms || !count) return fail(ADMM_EINVAL, "NULL argument");
-  HIP_TRY(hipSetDevice(c->device));
+  DEVICE_GUARD(c->device);
   for (int i = 0; i < ADMM_PROF_CLASSES; ++i) {
     ms[i] = 0.0;
     count[i] = 0;
@@ -582,7 +657,7 @@ int admm_profile_read(AdmmCtx* c, double* ms, int32_t* count) {
 
 int admm_get_stats(AdmmCtx* c, AdmmStats* out) {
   if (!c || !out) return fail(ADMM_EINVAL, "NULL argument");
-  HIP_TRY(hipSetDevice(c->device));
+  DEVICE_GUARD(c->device);
   DevStats d;
   HIP_TRY(hipDeviceSynchronize());
   HIP_TRY(hipMemcpy(&d, c->stats, sizeof d, hipMemcpyDeviceToHost));
@@ -608,7 +683,7 @@ int admm_debug_workspace(AdmmCtx* c, int32_t which, void* dst, int64_t bytes, vo
   if (bytes < need) return fail(ADMM_EINVAL, "admm_debug_workspace: %lld bytes < %lld", (long long)bytes, (long long)need);
   const float* src = which == 0 ? c->zc : which == 1 ? c->tgt : nullptr;
   if (!src) return fail(ADMM_EINVAL, "admm_debug_workspace: unknown array %d", which);
-  HIP_TRY(hipSetDevice(c->device));
+  DEVICE_GUARD(c->device);
   hipStream_t s = (hipStream_t)stream;
   HIP_TRY(hipMemcpyAsync(dst, src, need, hipMemcpyDeviceToDevice, s));
   HIP_TRY(hipStreamSynchronize(s));

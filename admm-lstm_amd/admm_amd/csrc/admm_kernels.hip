@@ -1920,14 +1920,22 @@ __device__ __forceinline__ float ht_theta_star(const Hyper& hp, const double* su
 template <int OC>
 __global__ __launch_bounds__(kThreads) void k_ht_apply(Geom g, Hyper hp, Planes6 S, Planes6 L, float* a, float* Ly,
                                                          const float* y, const float* wy, const double* sums,
-                                                         DevStats* stats) {
+                                                         DevStats* stats, int* status) {
   const int NO = OC > 0 ? OC : g.O;   // output width: compile-time for O = 1 (arrays stay in registers)
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const float ry = hp.rho[6], rh = hp.rho[5];
   const bool nd = hp.variant == 1;
   const bool shift = !nd && hp.with_dual_y;
   const float th = ht_theta_star(hp, sums);
-  if (blockIdx.x == 0 && threadIdx.x == 0) stats->theta_h = th;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    stats->theta_h = th;
+    if (status) {   // host-mapped mirror for admm_poll_status (the decide kernels ran earlier on this stream)
+      __hip_atomic_store(&status[0], __hip_atomic_load(&stats->unresolved, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      __hip_atomic_store(&status[1], __hip_atomic_load(&stats->nonfinite, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
   const int64_t rs = (int64_t)g.TP() * g.H, tofs = (int64_t)g.T * g.H;
   const float Bry = (float)g.Bg * ry;
   float sbuf[HT_W];
@@ -2247,9 +2255,9 @@ void launch_ht_reduce(const double* part, int nblk, double* sums, hipStream_t s)
 }
 
 void launch_ht_apply(const Geom& g, const Hyper& hp, const Planes6& S, const Planes6& L, float* a, float* Ly,
-                     const float* y, const float* wy, const double* sums, DevStats* stats, hipStream_t s) {
-  if (g.O == 1) k_ht_apply<1><<<ht_blocks(g), kThreads, 0, s>>>(g, hp, S, L, a, Ly, y, wy, sums, stats);
-  else k_ht_apply<0><<<ht_blocks(g), kThreads, 0, s>>>(g, hp, S, L, a, Ly, y, wy, sums, stats);
+                     const float* y, const float* wy, const double* sums, DevStats* stats, int* status, hipStream_t s) {
+  if (g.O == 1) k_ht_apply<1><<<ht_blocks(g), kThreads, 0, s>>>(g, hp, S, L, a, Ly, y, wy, sums, stats, status);
+  else k_ht_apply<0><<<ht_blocks(g), kThreads, 0, s>>>(g, hp, S, L, a, Ly, y, wy, sums, stats, status);
 }
 
 }  // namespace admm

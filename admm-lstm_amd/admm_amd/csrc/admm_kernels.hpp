@@ -204,6 +204,6 @@ void launch_ht_partial(const Geom& g, const Hyper& hp, const Planes6& S, const P
                        const float* Ly, const float* wy, double* part, int nblk, hipStream_t s);
 void launch_ht_reduce(const double* part, int nblk, double* sums, hipStream_t s);
 void launch_ht_apply(const Geom& g, const Hyper& hp, const Planes6& S, const Planes6& L, float* a, float* Ly,
-                     const float* y, const float* wy, const double* sums, DevStats* stats, hipStream_t s);
+                     const float* y, const float* wy, const double* sums, DevStats* stats, int* status, hipStream_t s);
 
 }  // namespace admm

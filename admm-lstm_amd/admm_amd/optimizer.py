@@ -185,6 +185,9 @@ class AdmmOptimizerBase(object):
 
     def _connect_comm(self) -> None:
         import torch.distributed as dist
+        if dist.get_backend() != 'nccl':
+            self._connect_host_comm()
+            return
         uid = ctypes.create_string_buffer(N.NCCL_UNIQUE_ID_BYTES)
         if self._rank == 0:
             N.check(self._lib.admm_comm_unique_id(uid, N.NCCL_UNIQUE_ID_BYTES), 'admm_comm_unique_id')
@@ -193,6 +196,27 @@ class AdmmOptimizerBase(object):
         raw = ctypes.create_string_buffer(box[0], N.NCCL_UNIQUE_ID_BYTES)
         N.check(self._lib.admm_set_comm(self._ctx, raw, N.NCCL_UNIQUE_ID_BYTES, self._rank, self._world),
                 'admm_set_comm')
+
+    def _connect_host_comm(self) -> None:
+        """Non-RCCL process groups (gloo): the library stages each all-reduce through host
+        memory and calls back here (``admm_set_comm_host``).  This is how the sharded step is
+        tested with several processes on one GPU; RCCL (``nccl`` backend) is the product path."""
+        import numpy as np
+        import torch.distributed as dist
+
+        def allreduce(buf, count, dtype, _user):
+            try:
+                ct = ctypes.c_float if dtype == 0 else ctypes.c_double
+                arr = np.ctypeslib.as_array(ctypes.cast(buf, ctypes.POINTER(ct)), shape=(int(count),))
+                t = torch.from_numpy(arr)   # shares the library's staging buffer
+                dist.all_reduce(t)
+                return 0
+            except Exception:  # pragma: no cover - reported by the library as ADMM_ECOMM
+                return 1
+
+        self._host_ar = N.HOST_ALLREDUCE_FN(allreduce)   # keep the thunk alive with the context
+        N.check(self._lib.admm_set_comm_host(self._ctx, self._host_ar, None, self._rank, self._world),
+                'admm_set_comm_host')
 
     # ------------------------------------------------------------------ bindings
     def _tensors(self):
@@ -237,8 +261,13 @@ class AdmmOptimizerBase(object):
             N.check(self._lib.admm_invalidate_cache(self._ctx), 'admm_invalidate_cache')
 
     def _cache_versions(self):
+        """In-place versions of every tensor the library's caches are derived from: the z
+        cache (x, the eight gate weights, h) and the x stage's targets tgt = dual/rho + gate
+        (the i, f, g, o gate and dual planes), plus c and the remaining duals, which the
+        library treats as known (dual h is zero before T unless the caller writes it)."""
         m = self.model
-        ts = [self._x] + [getattr(m, f'{s}2{q}') for s in 'xh' for q in GATES4] + [self.gates['h']]
+        ts = ([self._x] + [getattr(m, f'{s}2{q}') for s in 'xh' for q in GATES4]
+              + [self.gates[q] for q in GATES6] + [self.duals[q] for q in GATES6])
         return tuple(t._version for t in ts)
 
     def _snapshot(self) -> None:
@@ -255,6 +284,20 @@ class AdmmOptimizerBase(object):
         self._sync_bindings()
         N.check(self._lib.admm_step(self._ctx, N.stream_handle(self._device)), 'admm_step')
         self._snapshot()
+        self._poll_status()
+
+    def _poll_status(self) -> None:
+        """Warn (without a device sync) when a line search ran out of its exponent window
+        or saw non-finite objective values; the counts lag by the steps still in flight."""
+        unres, nonfin = ctypes.c_int32(), ctypes.c_int32()
+        N.check(self._lib.admm_poll_status(self._ctx, ctypes.byref(unres), ctypes.byref(nonfin)), 'admm_poll_status')
+        seen = getattr(self, '_status_seen', (0, 0))
+        if unres.value > seen[0]:
+            warning(f'{unres.value - seen[0]} weight line search(es) found no accepted exponent below 2^64 '
+                    f'(admm.py:334-336 would keep doubling); theta = 2^63 was applied (last_step_stats()).')
+        if nonfin.value > seen[1]:
+            warning(f'{nonfin.value - seen[1]} non-finite line-search objective value(s) seen.')
+        self._status_seen = (unres.value, nonfin.value)
 
     # ------------------------------------------------------------------ extras
     def last_step_stats(self) -> dict:

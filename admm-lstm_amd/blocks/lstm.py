@@ -88,8 +88,11 @@ class LSTM(nn.Module):
         out['c'] = c if c is not None else torch.zeros(B, T + 1, H, **kw)
         out['h'] = h if h is not None else torch.zeros(B, T + 1, H, **kw)
         for k in ('c', 'h'):
-            if not (out[k].is_contiguous() and out[k].dtype == torch.float32 and out[k].device == x.device):
-                raise ValueError(f'{k} must be a contiguous float32 [B,T+1,H] tensor on {x.device}')
+            # the library writes B rows with a row stride of (T+1)*H into these buffers
+            if not (tuple(out[k].shape) == (B, T + 1, H) and out[k].is_contiguous()
+                    and out[k].dtype == torch.float32 and out[k].device == x.device):
+                raise ValueError(f'{k} must be a contiguous float32 tensor of shape {(B, T + 1, H)} on '
+                                 f'{x.device} (got {tuple(out[k].shape)} {out[k].dtype} on {out[k].device})')
         a = torch.empty(B, O, **kw)
         xc = x.contiguous().float()
         wx, wh, wy = _weight_ptrs(self, x.device)

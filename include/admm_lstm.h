@@ -133,7 +133,22 @@ int admm_invalidate_cache(AdmmCtx* ctx);
 int admm_comm_unique_id(void* out, int64_t out_bytes);
 int admm_set_comm(AdmmCtx* ctx, const void* unique_id, int64_t id_bytes, int rank, int world);
 
+/* Host-staged communicator, for hosts without RCCL and for testing the sharded step with
+   several processes on one GPU (torch.distributed gloo): every all-reduce of admm_step
+   synchronises the stream, copies the buffer to host memory and calls fn, which must sum
+   `count` elements (dtype 0 = float32, 1 = float64) over all ranks in place and return 0.
+   Replaces any RCCL communicator.  Not the performance path: each call is a host round trip. */
+typedef int (*admm_host_allreduce_fn)(void* host_buf, int64_t count, int32_t dtype, void* user);
+int admm_set_comm_host(AdmmCtx* ctx, admm_host_allreduce_fn fn, void* user, int rank, int world);
+
+/* Synchronous: the diagnostics of the last step (line-search exponents etc.). */
 int admm_get_stats(AdmmCtx* ctx, AdmmStats* out);
+
+/* Non-blocking: the running counts of line searches that found no exponent in the
+   searched window (admm.py:334-336 would keep doubling) and of
+   non-finite objective values, as of the last step whose final kernel has completed
+   (a host-mapped mirror; no device sync).  The drop-in warns when they grow. */
+int admm_poll_status(AdmmCtx* ctx, int32_t* unresolved, int32_t* nonfinite);
 
 /* Live kernel timing (used by bench.py's roofline): when a class bit is set, admm_step
    records a hipEvent pair around every launch of that class on the step's stream.

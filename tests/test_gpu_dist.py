@@ -19,11 +19,30 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def test_rccl_world1_matches_single_process():
-    cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', '--nproc-per-node=1',
+def _launch(world, backend, shape, variant='admm'):
+    cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', f'--nproc-per-node={world}',
            '--master-addr=127.0.0.1', f'--master-port={_free_port()}',
            os.path.join(ROOT, 'tests', '_dist_worker.py')]
-    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY='0')
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY='0', ADMM_DIST_BACKEND=backend, ADMM_DIST_SHAPE=shape,
+               ADMM_DIST_VARIANT=variant, OMP_NUM_THREADS='4')
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env)
     out = r.stdout + r.stderr
     assert r.returncode == 0 and 'DIST OK' in out, out[-3000:]
+    print([ln for ln in out.splitlines() if 'DIST' in ln])
+
+
+def test_rccl_world1_matches_single_process():
+    _launch(1, 'nccl', '256,8,4,32')
+
+
+def test_rccl_world1_fast_path():
+    _launch(1, 'nccl', '512,6,16,256')
+
+
+@pytest.mark.parametrize('shape,variant', [
+    ('512,6,16,256', 'admm'),        # fast path: persistent sweep, split3, row-pair trials
+    ('200,5,16,64', 'admm'),         # persistent sweep at H = 64, ragged row blocks
+    ('96,4,3,40', 'no_dual_y'),      # generic kernels, the variant's h_T / wy forms
+])
+def test_host_comm_world2_matches_single_process(shape, variant):
+    _launch(2, 'gloo', shape, variant)

@@ -373,6 +373,75 @@ def test_external_weight_change_invalidates_cache(mods, dev):
         assert torch.equal(p.detach(), got[n]), n
 
 
+@pytest.mark.parametrize('edit', ["duals['i']", "gates['o']", "duals['c']"])
+def test_inplace_state_edit_invalidates_targets(edit, mods, dev):
+    """The persistent sweep leaves the x stage's targets tgt = dual/rho + gate in the
+    library (DESIGN.md "tgt from the sweep").  Editing a gate or dual plane in place
+    between steps (no new pointer, h and the weights untouched) must make the next step
+    read the live planes: it must equal a fresh optimizer started from the edited state."""
+    from blocks.lstm import LSTM
+    from parameters import example_parameter_dictionary
+    admm, _ = mods
+    admm.with_dual_y = False
+    B, T, D, H = 300, 3, 16, 64
+    g = torch.Generator().manual_seed(21)
+    x = torch.rand(B, T, D, generator=g).to(dev)
+    y = torch.rand(B, 1, generator=g).to(dev)
+    pd = example_parameter_dictionary['GoogleStock']
+    torch.manual_seed(0)
+    m = LSTM(D, H, 1).to(dev)
+    opt = admm.ADMMBasedOptimizer(m, (x, y), pd, verbose=False)
+    opt.step()
+    part, key = edit.split('[')
+    plane = getattr(opt, part)[key.strip("']")]
+    with torch.no_grad():
+        plane[:, 1:].add_(0.05 * torch.rand(plane[:, 1:].shape, generator=g).to(dev))
+    state = {k: v.clone() for k, v in opt.gates.items()}, {k: v.clone() for k, v in opt.duals.items()}
+    weights = {n: p.detach().clone() for n, p in m.named_parameters()}
+    opt.step()
+    torch.manual_seed(0)
+    m2 = LSTM(D, H, 1).to(dev)
+    opt2 = admm.ADMMBasedOptimizer(m2, (x, y), pd, verbose=False)
+    with torch.no_grad():
+        for n, p in m2.named_parameters():
+            p.copy_(weights[n])
+        for k, v in state[0].items():
+            opt2.gates[k].copy_(v)
+        for k, v in state[1].items():
+            opt2.duals[k].copy_(v)
+    opt2.step()
+    for n, p in m2.named_parameters():
+        assert torch.equal(p.detach(), dict(m.named_parameters())[n].detach()), n
+    assert list(opt.last_step_stats()['k'].values()) == list(opt2.last_step_stats()['k'].values())
+
+
+def test_init_gate_variables_rejects_wrong_state_shape(dev):
+    """Caller-supplied c / h buffers must be [B, T+1, H]: the library writes B rows of
+    stride (T+1)*H into them (blocks/lstm.py:65-88 indexes them as such)."""
+    from blocks.lstm import LSTM
+    torch.manual_seed(0)
+    m = LSTM(3, 8, 1).to(dev)
+    x = torch.rand(5, 4, 3, device=dev)
+    for bad in ((5, 8), (4, 5, 8), (5, 4, 8)):
+        with pytest.raises(ValueError):
+            m.init_gate_variables(x, c=torch.zeros(*bad, device=dev))
+    out = m.init_gate_variables(x, c=torch.zeros(5, 5, 8, device=dev), h=torch.zeros(5, 5, 8, device=dev))
+    assert out['h'].shape == (5, 5, 8)
+
+
+def test_poll_status_mirrors_stats(mods, dev):
+    """admm_poll_status (host-mapped, no sync) agrees with admm_get_stats once the device is idle."""
+    g = Golden('t0_admm')
+    model, opt = _optimizer(g, mods, dev)
+    for _ in range(2):
+        opt.step()
+    torch.cuda.synchronize()
+    st = opt.last_step_stats()
+    unres, nonfin = ctypes.c_int32(-1), ctypes.c_int32(-1)
+    assert opt._lib.admm_poll_status(opt._ctx, ctypes.byref(unres), ctypes.byref(nonfin)) == 0
+    assert (unres.value, nonfin.value) == (st['unresolved'], st['nonfinite'])
+
+
 def test_full_size_c3_properties(mods, dev):
     """BASELINE C3 size (B=8192, T=32, D=16, H=256): determinism (bitwise), finiteness,
     monotone loss over the first steps, and no unresolved line searches."""

@@ -93,6 +93,11 @@ struct AdmmCtx {
   int steps = 0;
   // workspace (all device)
   float *zc = nullptr, *tgt = nullptr, *R = nullptr, *Q = nullptr;  // [4][BT][H]
+  // speculative x-stage z update (SpecX, H % 256 == 0 fast path; ADMM_SPEC_X=0 disables):
+  // zx = zc + x dWx is written by pass 0 of the x trials for the predicted exponent
+  bool spec_x = false;
+  float* zx = nullptr;   // [4][BT][H], the h stage's z
+  int* kpred = nullptr;
   float *G = nullptr, *dW = nullptr, *gslab = nullptr;
   double *tr_part = nullptr, *tr_sums = nullptr, *tr_poly = nullptr;
   int nblk_resid = 1, nblk_trial = 1, nblk_rx = 1;
@@ -227,10 +232,15 @@ int stage_weights(AdmmCtx* c, int side, hipStream_t s) {
   const int Kd = side == 0 ? g.D : g.H;
   const bool fast = fast_path(g) && !c->force_generic;
   const Planes6 S = planes(c->buf.gates), L = planes(c->buf.duals);
-  if (fast && side == 1) {  // z of the h-side searches uses the updated x2q (admm.py:298-300)
+  const bool spec = fast && c->spec_x;
+  // z of the h-side searches uses the updated x2q (admm.py:298-300): zc += x dWx, or with
+  // speculation zx (written by the x trials) fixed up for mispredicted gates
+  if (fast && side == 1) {
     ProfScope ps(c, ADMM_PROF_RESID, s);
-    launch_apply_dwx(g, c->buf.x, c->dW, c->zc, s);
+    if (spec) launch_apply_fix(g, c->buf.x, c->dW, c->zc, c->zx, c->kpred, c->stats, s);
+    else launch_apply_dwx(g, c->buf.x, c->dW, c->zc, s);
   }
+  float* const zh = spec ? c->zx : c->zc;   // z of this stage's h side
   int ns;
   // 1. G_q = rho_q sum_rows A^T R_q
   if (fast && side == 0) {
@@ -240,11 +250,11 @@ int stage_weights(AdmmCtx* c, int side, hipStream_t s) {
   } else if (fast && c->split3) {
     ns = atr3_splits(g);
     ProfScope ps(c, ADMM_PROF_ATR_H, s);
-    launch_atr3(g, c->buf.gates[ADMM_H], c->zc, c->tgt, c->gslab, ns, s);
+    launch_atr3(g, c->buf.gates[ADMM_H], zh, c->tgt, c->gslab, ns, s);
   } else if (fast) {
     ns = atr_splits(g, 1);
     ProfScope ps(c, ADMM_PROF_ATR_H, s);
-    launch_atr_fused(g, c->hp, c->buf.x, c->buf.gates[ADMM_H], c->zc, c->tgt, c->dW, c->gslab, ns, s);
+    launch_atr_fused(g, c->hp, c->buf.x, c->buf.gates[ADMM_H], zh, c->tgt, c->dW, c->gslab, ns, s);
   } else {
     ResidArgs ra{};
     ra.stage = side;
@@ -264,7 +274,7 @@ int stage_weights(AdmmCtx* c, int side, hipStream_t s) {
     ProfScope ps(c, side == 0 ? ADMM_PROF_ATR_X : ADMM_PROF_ATR_H, s);
     launch_atr(g, side, c->buf.x, c->buf.gates[ADMM_H], c->R, c->gslab, ns, s);
   }
-  launch_reduce_g(g, side, c->hp, c->gslab, ns, c->G, c->found, s);
+  launch_reduce_g(g, side, c->hp, c->gslab, ns, c->G, c->found, spec && side == 0 ? c->kpred : nullptr, c->stats, s);
   int rc = allreduce_f32(c, c->G, (size_t)4 * Kd * g.H, s);
   if (rc) return rc;
   // 2. trial direction Q = A G (not needed on the fast x side: formed inside the trials)
@@ -291,9 +301,16 @@ int stage_weights(AdmmCtx* c, int side, hipStream_t s) {
   for (int pass = 0; pass < kMaxPasses; ++pass) {
     {
       ProfScope ps(c, pass == 0 ? ADMM_PROF_TRIAL : ADMM_PROF_TRIAL_EXTRA, s);
+      SpecX sx{};
+      if (spec && side == 0 && pass == 0) {
+        sx.kpred = c->kpred;
+        for (int q = 0; q < 4; ++q) sx.W[q] = c->buf.wx[q];
+        sx.zx = c->zx;
+        sx.hp = c->hp;
+      }
       if (fast)
-        launch_trial_fast(g, side, pass, c->zc, c->tgt, side == 1 ? c->Q : nullptr, c->buf.x,
-                          side == 0 ? c->G : c->dW, c->found, c->tr_part, nblk, s);
+        launch_trial_fast(g, side, pass, side == 1 ? zh : c->zc, c->tgt, side == 1 ? c->Q : nullptr, c->buf.x,
+                          side == 0 ? c->G : c->dW, c->found, c->tr_part, nblk, s, sx.zx ? &sx : nullptr);
       else
         launch_trial(g, pass, c->zc, c->tgt, c->Q, c->found, c->tr_part, nblk, s);
     }
@@ -411,6 +428,8 @@ int admm_create(const AdmmDims* dims, const AdmmParams* params, int device, Admm
   if (const char* e = std::getenv("ADMM_TGT_SWEEP")) c->tgt_sweep = std::atoi(e) != 0;
   if (const char* e = std::getenv("ADMM_GENERIC")) c->force_generic = std::atoi(e) != 0;
   c->split3 = fast_path(g) && split3_ok(g);
+  c->spec_x = fast_path(g) && trial_rows_ok(g);
+  if (const char* e = std::getenv("ADMM_SPEC_X")) c->spec_x = c->spec_x && std::atoi(e) != 0;
   if (const char* e = std::getenv("ADMM_SPLIT3")) c->split3 = c->split3 && std::atoi(e) != 0;
   Hyper& h = c->hp;
   for (int i = 0; i < 7; ++i) h.rho[i] = params->rho[i];
@@ -444,7 +463,8 @@ int admm_create(const AdmmDims* dims, const AdmmParams* params, int device, Admm
       (rc = dalloc(&c->Gy, (size_t)g.H * g.O)) || (rc = dalloc(&c->ht_part, (size_t)c->ht_nblk * kHTSums)) ||
       (rc = dalloc(&c->ht_sums, kHTSums)) || (rc = dalloc(&c->stats, 1)) ||
       (c->sweep_rows && (rc = dalloc(&c->swt, sweep_wt_floats(g)))) ||
-      (c->split3 && (rc = dalloc(&c->gimg, split3_gimg_floats(g))))) {
+      (c->split3 && (rc = dalloc(&c->gimg, split3_gimg_floats(g)))) ||
+      (c->spec_x && ((rc = dalloc(&c->zx, 4 * plane)) || (rc = dalloc(&c->kpred, 4))))) {
     std::string msg = g_last_error;
     admm_destroy(c);
     return fail(rc, "%s", msg.c_str());
@@ -475,7 +495,7 @@ int admm_destroy(AdmmCtx* c) {
   if (!c) return ADMM_OK;
   DeviceGuard dg_(c->device);
   void* ptrs[] = {c->zc, c->tgt, c->R, c->Q, c->G, c->dW, c->gslab, c->tr_part, c->tr_sums, c->tr_poly, c->found, c->pick,
-                  c->U, c->wy_slab, c->Gy, c->ht_part, c->ht_sums, c->stats, c->swt, c->gimg};
+                  c->U, c->wy_slab, c->Gy, c->ht_part, c->ht_sums, c->stats, c->swt, c->gimg, c->zx, c->kpred};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   if (c->comm) ncclCommDestroy(c->comm);

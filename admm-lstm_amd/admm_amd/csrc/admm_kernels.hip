@@ -812,10 +812,13 @@ __global__ __launch_bounds__(kThreads) void k_atr_fused(Geom g, const float* x, 
 }
 
 __global__ __launch_bounds__(kThreads) void k_reduce_g(int Kd, int H, Hyper hp, const float* slab, int nsplit,
-                                                         float* G, int* found) {
+                                                         float* G, int* found, int* kpred, const DevStats* stats) {
   const int64_t per_q = (int64_t)Kd * H;
   const int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x;
-  if (i < 4) found[i] = 0;   // this stage's line searches start undecided (no memset launch)
+  if (i < 4) {
+    found[i] = 0;   // this stage's line searches start undecided (no memset launch)
+    if (kpred) kpred[i] = stats->k[2 * i];   // last step's x-side exponent (SpecX)
+  }
   if (i >= 4 * per_q) return;
   const int q = (int)(i / per_q);
   // sequential fp64 sum over the splits (fixed order: deterministic), loads issued 8 at a time
@@ -1216,6 +1219,21 @@ __global__ __launch_bounds__(kThreads) void k_trial(Geom g, int pass, const floa
 // direction on the fly, q = x_row . G_x[:, j] (no Q buffer); side 1 applies the x-side
 // update to the cached pre-activations on the fly, z = zc + x_row . dWx[:, j].
 
+// W <- (0.5 rho T theta* W - G) / (beta + 0.5 rho theta* T), theta* = 2^k / 2 (admm.py:338-343):
+// one definition for k_wupdate and the speculative x-stage z update (SpecX), which must
+// reproduce its dWx bit for bit.
+struct WUpd {
+  float c1, den;
+  __device__ static WUpd make(float rho, float beta, int T, int pick) {
+    const float theta = ldexpf(1.f, pick - 1);
+    WUpd u;
+    u.c1 = ((0.5f * rho) * (float)T) * theta;
+    u.den = beta + ((0.5f * rho) * theta) * (float)T;
+    return u;
+  }
+  __device__ float apply(float w0, float G) const { return fmaf(c1, w0, -G) / den; }
+};
+
 struct RowCols {  // thread -> (row offset, float4 column) of a rows x (H/4) grid
   int tpr, rpb, rr, c4;
   __device__ RowCols(int H) {
@@ -1259,9 +1277,10 @@ template <int DP>
 __device__ __forceinline__ float4 xw_row(const float (&xr)[DP], const float4* __restrict__ wl4, int H4, int c4) {
   float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
-  for (int d = 0; d < DP; ++d) {
+  for (int d = 0; d < DP; ++d) {   // explicit fmas: the speculative update (SpecX) uses the same order
     const float4 wv = wl4[d * H4 + c4];
-    acc.x += xr[d] * wv.x; acc.y += xr[d] * wv.y; acc.z += xr[d] * wv.z; acc.w += xr[d] * wv.w;
+    acc.x = fmaf(xr[d], wv.x, acc.x); acc.y = fmaf(xr[d], wv.y, acc.y);
+    acc.z = fmaf(xr[d], wv.z, acc.z); acc.w = fmaf(xr[d], wv.w, acc.w);
   }
   return acc;
 }
@@ -1372,11 +1391,12 @@ __global__ __launch_bounds__(kThreads, TF_MINB) void k_trial_fast(Geom g, int pa
 // VGPRs for the whole pass: q = x_row . G_x costs 16 FMAs and no LDS.  The two rows are the two
 // halves of trial_pair's packed arithmetic; the next pair's operands are loaded while this one
 // is evaluated.  Side 1 reads q from Q instead.
-template <bool TANH, int SIDE, int DP, bool XV>
+template <bool TANH, int SIDE, int DP, bool XV, bool SPEC>
 __device__ __forceinline__ void trial_rows_body(const Geom& g, int q, int pass, const float* __restrict__ zc,
                                                 const float* __restrict__ tgt, const float* __restrict__ Q,
                                                 const float* __restrict__ x, const float* __restrict__ Gx, int blk,
-                                                int nblk, float (&acc)[kSlots], DirectQ& dq) {
+                                                int nblk, float (&acc)[kSlots], DirectQ& dq, const SpecX& sp,
+                                                float4* dwl) {
   const int64_t BT = g.BT(), n = BT * g.H;
   const int j = blockIdx.z * 256 + threadIdx.x;
   const float* __restrict__ zq = zc + (int64_t)q * n + j;
@@ -1385,6 +1405,24 @@ __device__ __forceinline__ void trial_rows_body(const Geom& g, int q, int pass, 
   float gw[DP];
 #pragma unroll
   for (int d = 0; d < DP; ++d) gw[d] = (SIDE == 0 && d < g.D) ? Gx[((int64_t)q * g.D + d) * g.H + j] : 0.f;
+  // SPEC: this column of dWx for the predicted exponent, as k_wupdate will form it, parked in
+  // LDS as [DP/4][256] float4 (each thread reads back only its own column: no barrier) so the
+  // kernel keeps its 4 waves per SIMD
+  float* __restrict__ zxq = SPEC ? sp.zx + (int64_t)q * n + j : nullptr;
+  if constexpr (SPEC) {
+    const WUpd u = WUpd::make(sp.hp.rho[q], sp.hp.beta_x[q], g.T, sp.kpred[q]);
+#pragma unroll
+    for (int d4 = 0; d4 < DP / 4; ++d4) {
+      float v[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int d = 4 * d4 + e;
+        const float w0 = d < g.D ? sp.W[q][(int64_t)d * g.H + j] : 0.f;
+        v[e] = d < g.D ? u.apply(w0, gw[d]) - w0 : 0.f;
+      }
+      dwl[d4 * 256 + threadIdx.x] = make_float4(v[0], v[1], v[2], v[3]);
+    }
+  }
   struct In { f32x2 z, t, q; float xa[DP], xb[DP]; };
   auto load = [&](int64_t ra, In& v) {   // rows ra, ra + 1 (clamped)
     const int64_t r0 = __builtin_amdgcn_readfirstlane((int)(ra < BT ? ra : BT - 1));
@@ -1416,6 +1454,27 @@ __device__ __forceinline__ void trial_rows_body(const Geom& g, int q, int pass, 
         qb = fmaf(cur.xb[d], gw[d], qb);
       }
       qv = f32x2{qa, qb};
+      if constexpr (SPEC) {   // z + x dWx in k_apply_dwx's order (xw_row)
+        // an opaque zero offset keeps the LDS reads inside the loop (hoisted, they would take
+        // 16 VGPRs for the whole pass)
+        int zo;
+        asm volatile("v_mov_b32 %0, 0" : "=v"(zo));
+        const float4* dl = dwl + zo + threadIdx.x;
+        float da = 0.f, db = 0.f;
+#pragma unroll
+        for (int d4 = 0; d4 < DP / 4; ++d4) {
+          const float4 w = dl[d4 * 256];
+          const float wv[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            da = fmaf(cur.xa[4 * d4 + e], wv[e], da);
+            db = fmaf(cur.xb[4 * d4 + e], wv[e], db);
+          }
+        }
+        const int64_t r0 = __builtin_amdgcn_readfirstlane((int)base);
+        __builtin_nontemporal_store(cur.z.x + da, zxq + r0 * g.H);
+        if (base + 1 < BT) __builtin_nontemporal_store(cur.z.y + db, zxq + (r0 + 1) * g.H);
+      }
     }
     // row base + 1 may be past the end (odd BT): masked through its q and d0 (ok covers the pair)
     const bool ok1 = base + 1 < BT;
@@ -1428,36 +1487,43 @@ __device__ __forceinline__ void trial_rows_body(const Geom& g, int q, int pass, 
   dq_run(dq, acc, true);
 }
 
-template <int SIDE, int DP, bool XV>
+template <int SIDE, int DP, bool XV, bool SPEC>
 __global__ __launch_bounds__(kThreads) void k_trial_rows(Geom g, int pass, const float* __restrict__ zc,
                                                          const float* __restrict__ tgt, const float* __restrict__ Q,
                                                          const float* __restrict__ x, const float* __restrict__ Gx,
                                                          const int* __restrict__ found, double* __restrict__ part,
-                                                         int nblk) {
+                                                         int nblk, SpecX sp) {
   const int q = blockIdx.y, blk = blockIdx.x;
   if (found[q]) return;
   float acc[kSlots];
 #pragma unroll
   for (int k = 0; k < kSlots; ++k) acc[k] = 0.f;
   __shared__ float dqbuf[kThreads / 64][5 * kDQ];
+  __shared__ float4 dwl[SPEC ? DP / 4 * 256 : 1];
   DirectQ dq{dqbuf[threadIdx.x >> 6], 0, 0};
-  if (q == 2) trial_rows_body<true, SIDE, DP, XV>(g, q, pass, zc, tgt, Q, x, Gx, blk, nblk, acc, dq);
-  else trial_rows_body<false, SIDE, DP, XV>(g, q, pass, zc, tgt, Q, x, Gx, blk, nblk, acc, dq);
+  if (q == 2) trial_rows_body<true, SIDE, DP, XV, SPEC>(g, q, pass, zc, tgt, Q, x, Gx, blk, nblk, acc, dq, sp, dwl);
+  else trial_rows_body<false, SIDE, DP, XV, SPEC>(g, q, pass, zc, tgt, Q, x, Gx, blk, nblk, acc, dq, sp, dwl);
   // the column blocks of one (blk, q) add into the same part slot row: blk index widened by z
   trial_block_store(acc, part, q, blockIdx.z * nblk + blk, nblk * gridDim.z);
 }
 
 // After the x stage: zc += X dWx, so the h stage sees z = X Wx_new + Hprev Wh
 // (admm.py:298-300: the h-side search uses the already-updated x2q).
+// k_apply_fix (kpred != nullptr): zx = zc + X dWx, only for the gates whose decided x-side
+// exponent differs from the one pass 0 of the trials assumed (SpecX).
 template <int DP, bool XV>
 __global__ __launch_bounds__(kThreads) void k_apply_dwx(Geom g, const float* __restrict__ x,
-                                                          const float* __restrict__ dW, float* __restrict__ zc) {
+                                                          const float* __restrict__ dW, const float* zsrc,
+                                                          float* zdst, const int* __restrict__ kpred,
+                                                          const DevStats* __restrict__ stats) {
   extern __shared__ float wl[];  // [DP][H] of gate q
   const int q = blockIdx.y;
+  if (kpred && stats->k[2 * q] == kpred[q]) return;
   stage_wlds<DP>(g, dW + (int64_t)q * g.D * g.H, wl);
   const float4* __restrict__ wl4 = reinterpret_cast<const float4*>(wl);
   const int64_t BT = g.BT();
-  float* __restrict__ zq = zc + (int64_t)q * BT * g.H;
+  const float* zq = zsrc + (int64_t)q * BT * g.H;
+  float* zo = zdst + (int64_t)q * BT * g.H;
   RowCols rc(g.H);
   if (rc.rr >= rc.rpb) return;
   const int j = 4 * rc.c4, H4 = g.H / 4;
@@ -1480,7 +1546,7 @@ __global__ __launch_bounds__(kThreads) void k_apply_dwx(Geom g, const float* __r
       const float4 dz = xw_row<DP>(xr[r], wl4, H4, rc.c4);
       float4 zn;
       zn.x = z4[r].x + dz.x; zn.y = z4[r].y + dz.y; zn.z = z4[r].z + dz.z; zn.w = z4[r].w + dz.w;
-      st_nt(zq + row * g.H + j, zn);
+      st_nt(zo + row * g.H + j, zn);
     }
   }
 }
@@ -1704,14 +1770,12 @@ __global__ __launch_bounds__(kThreads) void k_wupdate(Geom g, Hyper hp, SelectAr
   const int64_t nW = (int64_t)Kd * g.H;
   const float* Gq = a.G + (int64_t)q * nW;
   const float rho = hp.rho[q];
-  const float theta = ldexpf(1.f, pick - 1);
   const float beta = a.side == 0 ? hp.beta_x[q] : hp.beta_h[q];
-  const float c1 = ((0.5f * rho) * (float)g.T) * theta;
-  const float den = beta + ((0.5f * rho) * theta) * (float)g.T;
+  const WUpd u = WUpd::make(rho, beta, g.T, pick);
   float* W = a.W[q];
   for (int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x; i < nW; i += (int64_t)gridDim.x * kThreads) {
     const float w0 = W[i];
-    const float w1 = (c1 * w0 - Gq[i]) / den;
+    const float w1 = u.apply(w0, Gq[i]);
     W[i] = w1;
     if (a.dW) a.dW[(int64_t)q * nW + i] = w1 - w0;
   }
@@ -2088,10 +2152,10 @@ void launch_atr(const Geom& g, int side, const float* x, const float* Sh, const 
 }
 
 void launch_reduce_g(const Geom& g, int side, const Hyper& hp, const float* slab, int nsplit, float* G, int* found,
-                     hipStream_t s) {
+                     int* kpred, const DevStats* stats, hipStream_t s) {
   const int Kd = side == 0 ? g.D : g.H;
   const int64_t n = 4LL * Kd * g.H;
-  k_reduce_g<<<cdiv64(n, kThreads), kThreads, 0, s>>>(Kd, g.H, hp, slab, nsplit, G, found);
+  k_reduce_g<<<cdiv64(n, kThreads), kThreads, 0, s>>>(Kd, g.H, hp, slab, nsplit, G, found, kpred, stats);
 }
 
 void launch_qgemm(const Geom& g, int side, const float* x, const float* Sh, const float* G, float* Q,
@@ -2170,18 +2234,30 @@ int stream_blocks(const Geom& g) {   // streaming passes: ~2 rows in flight per 
 void launch_apply_dwx(const Geom& g, const float* x, const float* dW, float* zc, hipStream_t s) {
   dim3 grid(stream_blocks(g), 4);
   with_dp(g, [&](auto dp, auto xv) {
-    k_apply_dwx<decltype(dp)::value, decltype(xv)::value><<<grid, kThreads, fast_lds(g), s>>>(g, x, dW, zc);
+    k_apply_dwx<decltype(dp)::value, decltype(xv)::value>
+        <<<grid, kThreads, fast_lds(g), s>>>(g, x, dW, zc, zc, nullptr, nullptr);
+  });
+}
+
+void launch_apply_fix(const Geom& g, const float* x, const float* dW, const float* zc, float* zx, const int* kpred,
+                      const DevStats* stats, hipStream_t s) {
+  dim3 grid(stream_blocks(g), 4);
+  with_dp(g, [&](auto dp, auto xv) {
+    k_apply_dwx<decltype(dp)::value, decltype(xv)::value>
+        <<<grid, kThreads, fast_lds(g), s>>>(g, x, dW, zc, zx, kpred, stats);
   });
 }
 
 bool trial_rows_ok(const Geom& g) { return g.H % 256 == 0; }
 
 void launch_trial_fast(const Geom& g, int side, int pass, const float* zc, const float* tgt, const float* Q,
-                       const float* x, const float* Wsrc, const int* found, double* part, int nblk, hipStream_t s) {
+                       const float* x, const float* Wsrc, const int* found, double* part, int nblk, hipStream_t s,
+                       const SpecX* spec) {
   dim3 grid(nblk, 4);
+  const SpecX sp = spec ? *spec : SpecX{};
   if (side == 1 && trial_rows_ok(g)) {
     dim3 gr(nblk, 4, g.H / 256);
-    k_trial_rows<1, 4, false><<<gr, kThreads, 0, s>>>(g, pass, zc, tgt, Q, x, Wsrc, found, part, nblk);
+    k_trial_rows<1, 4, false, false><<<gr, kThreads, 0, s>>>(g, pass, zc, tgt, Q, x, Wsrc, found, part, nblk, sp);
     return;
   }
   if (side == 1) {  // no x . W product on this side: one instantiation
@@ -2191,8 +2267,12 @@ void launch_trial_fast(const Geom& g, int side, int pass, const float* zc, const
   if (trial_rows_ok(g)) {
     dim3 gr(nblk, 4, g.H / 256);
     with_dp(g, [&](auto dp, auto xv) {
-      k_trial_rows<0, decltype(dp)::value, decltype(xv)::value>
-          <<<gr, kThreads, 0, s>>>(g, pass, zc, tgt, Q, x, Wsrc, found, part, nblk);
+      if (spec)
+        k_trial_rows<0, decltype(dp)::value, decltype(xv)::value, true>
+            <<<gr, kThreads, 0, s>>>(g, pass, zc, tgt, Q, x, Wsrc, found, part, nblk, sp);
+      else
+        k_trial_rows<0, decltype(dp)::value, decltype(xv)::value, false>
+            <<<gr, kThreads, 0, s>>>(g, pass, zc, tgt, Q, x, Wsrc, found, part, nblk, sp);
     });
     return;
   }

@@ -126,7 +126,9 @@ int atr_splits(const Geom& g, int side);
 void launch_atr(const Geom& g, int side, const float* x, const float* Sh, const float* R, float* Gslab,
                 int nsplit, hipStream_t s);
 // G[q][m][j] = rho_q * sum_split Gslab; also clears found[0..3] for the stage's line searches
+// kpred (nullable, side 0): receives the previous step's x-side exponents from stats (SpecX)
 void launch_reduce_g(const Geom& g, int side, const Hyper& hp, const float* Gslab, int nsplit, float* G, int* found,
+                     int* kpred, const DevStats* stats,
                      hipStream_t s);
 // Q[q][row][j] = sum_m A[row][m] * G[q][m][j]
 void launch_qgemm(const Geom& g, int side, const float* x, const float* Sh, const float* G, float* Q,
@@ -152,8 +154,22 @@ int resid_gx_blocks(const Geom& g);
 void launch_resid_gx(const Geom& g, const Hyper& hp, const float* x, const Planes6& S, const Planes6& L,
                      const float* zc, float* tgt, float* slab, int nblk, bool tgt_ready, hipStream_t s);
 // trial pass without a materialised Q (side 0: q = x.G_x) or z (side 1: z = zc + x.dWx)
+// Speculative Gauss-Seidel z update of the x stage (H % 256 == 0): pass 0 of the x-side trials
+// also writes zx = zc + x dWx(kpred) for the exponent the gate took in the previous step
+// (kpred, copied from the stats by k_reduce_g), with dWx formed exactly as k_wupdate forms it;
+// k_apply_fix recomputes zx only for the gates whose decided exponent differs.
+struct SpecX {
+  const int* kpred;         // [4] predicted x-side exponent per gate
+  const float* W[4];        // x2q before the update
+  float* zx;                // [4][BT][H] z of the h stage (zc + x dWx)
+  Hyper hp;
+};
 void launch_trial_fast(const Geom& g, int side, int pass, const float* zc, const float* tgt, const float* Q,
-                       const float* x, const float* Wsrc, const int* found, double* part, int nblk, hipStream_t s);
+                       const float* x, const float* Wsrc, const int* found, double* part, int nblk, hipStream_t s,
+                       const SpecX* spec = nullptr);
+// after the x decision: zx = zc + X dWx for the gates whose exponent was mispredicted
+void launch_apply_fix(const Geom& g, const float* x, const float* dW, const float* zc, float* zx, const int* kpred,
+                      const DevStats* stats, hipStream_t s);
 int stream_blocks(const Geom& g);   // grid (per gate) of the fast streaming passes
 // H % 256 == 0: the fast trial passes run as row-pair workgroups over H/256 column blocks, and
 // write stream_blocks(g) * H/256 partials per slot (the reduce's nblk)

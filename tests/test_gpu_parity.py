@@ -633,6 +633,40 @@ def test_tgt_from_sweep_bit_identical(shape, mods, dev, monkeypatch):
     assert torch.equal(out[0][1], out[1][1])
 
 
+@pytest.mark.parametrize('shape,D_', [((300, 3, 256), 16), ((257, 4, 256), 5), ((130, 3, 512), 1)])
+def test_speculative_x_update_bit_identical(shape, D_, mods, dev, monkeypatch):
+    """SpecX (H % 256 == 0): pass 0 of the x-side trials writes z + x dWx for last step's
+    exponent and k_apply_fix redoes only mispredicted gates.  Steps 1-2 mispredict (k moves
+    from 0 to its working value), later steps hit; both must give the trajectory of the plain
+    apply (ADMM_SPEC_X=0) bit for bit, line-search exponents included.  Odd B*T covers the
+    unpaired last row; D = 5 and 1 the padded x rows."""
+    from blocks.lstm import LSTM
+    from parameters import example_parameter_dictionary
+    admm, _ = mods
+    admm.with_dual_y = False
+    B, T, H = shape
+    g = torch.Generator().manual_seed(13)
+    x = torch.rand(B, T, D_, generator=g).to(dev)
+    y = torch.rand(B, 1, generator=g).to(dev)
+    out = []
+    for mode in ('0', '1'):
+        monkeypatch.setenv('ADMM_SPEC_X', mode)
+        torch.manual_seed(0)
+        m = LSTM(D_, H, 1).to(dev)
+        opt = admm.ADMMBasedOptimizer(m, (x, y), example_parameter_dictionary['GoogleStock'], verbose=False)
+        ks = []
+        for _ in range(5):
+            opt.step()
+            ks.append(list(opt.last_step_stats()['k'].values()))
+        out.append((ks, torch.cat([p.detach().flatten() for p in m.parameters()]),
+                    torch.cat([v.flatten() for v in opt.gates.values()] + [v.flatten() for v in opt.duals.values()])))
+        del opt
+    assert out[0][0] == out[1][0]
+    assert torch.isfinite(out[1][1]).all()
+    assert torch.equal(out[0][1], out[1][1])
+    assert torch.equal(out[0][2], out[1][2])
+
+
 def test_generic_weight_stage_matches_fast(mods, dev, monkeypatch):
     """ADMM_GENERIC=1 runs the weight stages on the generic kernels (materialised R and Q, f32 MFMA
     GEMMs) instead of the fast streaming path.  Step 1 decides identically on both: the x-side

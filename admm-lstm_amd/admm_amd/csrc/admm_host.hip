@@ -90,6 +90,12 @@ struct AdmmCtx {
   // the persistent sweep writes tgt for the next x stage, which then reads it instead of
   // recomputing it from the gate and dual planes (ADMM_TGT_SWEEP=0 disables)
   bool tgt_sweep = true;
+  // ... and the next x stage's X^T R partials (k_sweep_rows GX, D <= 16), so that stage skips
+  // k_resid_gx (ADMM_GX_SWEEP=0 disables)
+  bool gx_sweep = true;
+  bool gx_valid = false;
+  float* gx_slab = nullptr;   // [sweep blocks][4][D][H]
+  int gx_nblk = 0;
   int steps = 0;
   // workspace (all device)
   float *zc = nullptr, *tgt = nullptr, *R = nullptr, *Q = nullptr;  // [4][BT][H]
@@ -243,7 +249,11 @@ int stage_weights(AdmmCtx* c, int side, hipStream_t s) {
   float* const zh = spec ? c->zx : c->zc;   // z of this stage's h side
   int ns;
   // 1. G_q = rho_q sum_rows A^T R_q
-  if (fast && side == 0) {
+  const float* gsrc = c->gslab;
+  if (fast && side == 0 && c->gx_valid && c->tgt_valid && c->z_valid) {
+    ns = c->gx_nblk;        // the sweep left the partials (and tgt) of this state
+    gsrc = c->gx_slab;
+  } else if (fast && side == 0) {
     ns = c->nblk_rx;
     ProfScope ps(c, ADMM_PROF_RESID, s);
     launch_resid_gx(g, c->hp, c->buf.x, S, L, c->zc, c->tgt, c->gslab, ns, c->tgt_valid && c->z_valid, s);
@@ -274,7 +284,7 @@ int stage_weights(AdmmCtx* c, int side, hipStream_t s) {
     ProfScope ps(c, side == 0 ? ADMM_PROF_ATR_X : ADMM_PROF_ATR_H, s);
     launch_atr(g, side, c->buf.x, c->buf.gates[ADMM_H], c->R, c->gslab, ns, s);
   }
-  launch_reduce_g(g, side, c->hp, c->gslab, ns, c->G, c->found, spec && side == 0 ? c->kpred : nullptr, c->stats, s);
+  launch_reduce_g(g, side, c->hp, gsrc, ns, c->G, c->found, spec && side == 0 ? c->kpred : nullptr, c->stats, s);
   int rc = allreduce_f32(c, c->G, (size_t)4 * Kd * g.H, s);
   if (rc) return rc;
   // 2. trial direction Q = A G (not needed on the fast x side: formed inside the trials)
@@ -337,6 +347,7 @@ int stage_sweep(AdmmCtx* c, hipStream_t s) {
     sa.r0 = 0;
     sa.r1 = g.B;
     sa.tgt = fast_path(g) && c->tgt_sweep ? c->tgt : nullptr;   // the fast x stage reads it next step
+    sa.gx_slab = sa.tgt ? c->gx_slab : nullptr;
     launch_sweep_wt(g, w, c->swt, s);
     launch_sweep_rows(g, c->swt, c->hp, sa, s);
   } else {
@@ -426,6 +437,7 @@ int admm_create(const AdmmDims* dims, const AdmmParams* params, int device, Admm
   c->sweep_rows = sweep_rows_ok(g);
   if (const char* e = std::getenv("ADMM_SWEEP_ROWS")) c->sweep_rows = c->sweep_rows && std::atoi(e) != 0;
   if (const char* e = std::getenv("ADMM_TGT_SWEEP")) c->tgt_sweep = std::atoi(e) != 0;
+  if (const char* e = std::getenv("ADMM_GX_SWEEP")) c->gx_sweep = std::atoi(e) != 0;
   if (const char* e = std::getenv("ADMM_GENERIC")) c->force_generic = std::atoi(e) != 0;
   c->split3 = fast_path(g) && split3_ok(g);
   c->spec_x = fast_path(g) && trial_rows_ok(g);
@@ -442,6 +454,8 @@ int admm_create(const AdmmDims* dims, const AdmmParams* params, int device, Admm
   h.with_dual_y = params->with_dual_y;
 
   const size_t plane = (size_t)g.BT() * g.H;
+  // the sweep's x-stage partials: persistent sweep, fast path, D <= 16, targets from the sweep
+  c->gx_nblk = c->sweep_rows && fast_path(g) && c->tgt_sweep && c->gx_sweep && g.D <= 16 ? (int)((g.B + 31) / 32) : 0;
   const int Kmax = g.D > g.H ? g.D : g.H;
   c->nblk_resid = resid_blocks(g);
   c->nblk_trial = std::max(trial_blocks(g), stream_blocks(g) * (trial_rows_ok(g) ? g.H / 256 : 1));
@@ -464,7 +478,8 @@ int admm_create(const AdmmDims* dims, const AdmmParams* params, int device, Admm
       (rc = dalloc(&c->ht_sums, kHTSums)) || (rc = dalloc(&c->stats, 1)) ||
       (c->sweep_rows && (rc = dalloc(&c->swt, sweep_wt_floats(g)))) ||
       (c->split3 && (rc = dalloc(&c->gimg, split3_gimg_floats(g)))) ||
-      (c->spec_x && ((rc = dalloc(&c->zx, 4 * plane)) || (rc = dalloc(&c->kpred, 4))))) {
+      (c->spec_x && ((rc = dalloc(&c->zx, 4 * plane)) || (rc = dalloc(&c->kpred, 4)))) ||
+      (c->gx_nblk > 0 && (rc = dalloc(&c->gx_slab, (size_t)c->gx_nblk * 4 * g.D * g.H)))) {
     std::string msg = g_last_error;
     admm_destroy(c);
     return fail(rc, "%s", msg.c_str());
@@ -495,7 +510,7 @@ int admm_destroy(AdmmCtx* c) {
   if (!c) return ADMM_OK;
   DeviceGuard dg_(c->device);
   void* ptrs[] = {c->zc, c->tgt, c->R, c->Q, c->G, c->dW, c->gslab, c->tr_part, c->tr_sums, c->tr_poly, c->found, c->pick,
-                  c->U, c->wy_slab, c->Gy, c->ht_part, c->ht_sums, c->stats, c->swt, c->gimg, c->zx, c->kpred};
+                  c->U, c->wy_slab, c->Gy, c->ht_part, c->ht_sums, c->stats, c->swt, c->gimg, c->zx, c->kpred, c->gx_slab};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   if (c->comm) ncclCommDestroy(c->comm);
@@ -527,6 +542,7 @@ int admm_bind(AdmmCtx* c, const AdmmBuffers* b) {
   c->bound = true;
   c->z_valid = false;
   c->tgt_valid = false;
+  c->gx_valid = false;
   return ADMM_OK;
 }
 
@@ -540,6 +556,7 @@ int admm_invalidate_cache(AdmmCtx* c) {
   if (!c) return fail(ADMM_EINVAL, "NULL ctx");
   c->z_valid = false;
   c->tgt_valid = false;
+  c->gx_valid = false;
   return ADMM_OK;
 }
 
@@ -577,6 +594,7 @@ int admm_init_state(AdmmCtx* c, void* stream) {
   HIP_TRY(hipGetLastError());
   c->z_valid = true;
   c->tgt_valid = false;   // recomputed from the new state by the first x stage
+  c->gx_valid = false;
   return ADMM_OK;
 }
 
@@ -597,6 +615,7 @@ int admm_step(AdmmCtx* c, void* stream) {
   HIP_TRY(hipGetLastError());
   c->z_valid = true;  // the sweep left x_t Wx + h_{t-1} Wh of the final state in the cache
   c->tgt_valid = c->sweep_rows && fast_path(c->g) && c->tgt_sweep;
+  c->gx_valid = c->tgt_valid && c->gx_slab != nullptr;
   c->steps++;
   return ADMM_OK;
 }

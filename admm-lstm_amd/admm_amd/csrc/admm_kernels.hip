@@ -150,19 +150,24 @@ struct SweepIn {
   float li, lf, lg, lo, lc, lh;
 };
 // sigma(z) for the sweep: accurate expf, 1/(1+e) by v_rcp and one Newton step (div_fast)
-__device__ __forceinline__ float sig_sweep(float z) {
+__device__ __forceinline__ SigPair sig_sweep2(float z) {   // sigma(z) and 1 - sigma(z) without cancellation
   const float e = expf(-fabsf(z));
   const float r = div_fast(1.f, 1.f + e);
-  return z >= 0.f ? r : e * r;
+  const float er = e * r;
+  return z >= 0.f ? SigPair{r, er} : SigPair{er, r};
 }
 struct SweepRes {
   float i1, f1, g1, o1, c1, h1;
   float li, lf, lg, lo, lc;
+  // phi'(z) of the four pre-activations (the next x stage's residual, k_sweep_rows GX)
+  float di, df, dg, dO;
+  float ai, af, ag, ao;    // phi(z)
 };
 
 __device__ __forceinline__ SweepRes sweep_point(const Hyper& hp, const SweepIn& v, bool last) {
   const float ri = hp.rho[0], rf = hp.rho[1], rg = hp.rho[2], ro = hp.rho[3], rc = hp.rho[4], rh = hp.rho[5];
-  const float ai = sig_sweep(v.zi), af = sig_sweep(v.zf), ag = tanhf(v.zg), ao = sig_sweep(v.zo);
+  const SigPair pi = sig_sweep2(v.zi), pf = sig_sweep2(v.zf), po = sig_sweep2(v.zo);
+  const float ai = pi.s, af = pf.s, ag = tanhf(v.zg), ao = po.s;
   const float f0 = v.f0, g0 = v.g0, c0 = v.c0, h0 = v.h0, cp = v.cp;
   const float li = v.li, lf = v.lf, lg = v.lg, lo = v.lo, lc = v.lc, lh = v.lh;
   SweepRes o;
@@ -185,6 +190,8 @@ __device__ __forceinline__ SweepRes sweep_point(const Hyper& hp, const SweepIn& 
   o.lg = lg + rg * (o.g1 - ag);
   o.lo = lo + ro * (o.o1 - ao);
   o.lc = lc + rc * (o.c1 - (o.f1 * cp + o.i1 * o.g1));
+  o.ai = ai; o.af = af; o.ag = ag; o.ao = ao;
+  o.di = pi.s * pi.sc; o.df = pf.s * pf.sc; o.dg = 1.f - ag * ag; o.dO = po.s * po.sc;
   return o;
 }
 
@@ -308,7 +315,13 @@ __global__ __launch_bounds__(kThreads) void k_sweep_wt(int D, int H, int XC, Wei
   }
 }
 
-template <int NT, int XC>
+// GX (D <= 16): the sweep also forms the next step's x-stage gradient partials
+// slab[blk][q][d][j] = sum_{its rows, t} x_t[row][d] R_q[row][j], R_q = (phi(z) - tgt) phi'(z) of
+// the new state (admm.py:302-312, x side), so that x stage needs no residual pass.  The consumer
+// leaves R of its tile in the z tile's LDS slot; two steps later the gate's producer wave folds
+// it in with 16 v_mfma_f32_16x16x4_f32 (K = the tile's 32 rows, M = d, N = 32 columns) into a
+// register ring of NT column tiles that turns once per tile.
+template <int NT, int XC, bool GX>
 __global__ __launch_bounds__(SR_THREADS) void k_sweep_rows(Geom g, const bf16x8* __restrict__ wt, Hyper hp,
                                                             SweepT a) {
   using SG = SrGeom<NT, XC>;
@@ -352,6 +365,46 @@ __global__ __launch_bounds__(SR_THREADS) void k_sweep_rows(Geom g, const bf16x8*
 #pragma unroll
       for (int p = 0; p < 3; ++p) bq[u][p] = wq[(u * 3 + p) * 64];
     f32x16 acc = {};
+    // GX: ring of the gate's G_x partials, slot 0 = the column tile folded next
+    f32x4 gx[NT][2];
+    float xcur[8], xnext[8];
+    int gxs = 0;   // tiles folded so far
+    auto load_gx_x = [&](int tn, float (&xv)[8]) {   // A operand: x_tn[row 4ks + lane/16][d = lane%16]
+#pragma unroll
+      for (int ks = 0; ks < 8; ++ks) {
+        const int64_t b = min(m0 + 4 * ks + (lane >> 4), a.r1 - 1);
+        const int d = lane & 15;
+        xv[ks] = d < D ? a.x[(b * T + (tn - 1)) * D + d] : 0.f;
+      }
+    };
+    auto gx_fold = [&](int buf) {   // R of the tile folded next, from Zb[buf]
+      if ((gxs % NT) == 0) {
+#pragma unroll
+        for (int ks = 0; ks < 8; ++ks) xcur[ks] = xnext[ks];
+        const int tn = gxs / NT + 2;
+        if (tn <= T) load_gx_x(tn, xnext);
+      }
+      const float* Rq = &Zb[buf][q * SR_ROWS * 32 + (lane >> 4) * 32 + (lane & 15)];
+#pragma unroll
+      for (int ks = 0; ks < 8; ++ks)
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+          gx[0][h] = __builtin_amdgcn_mfma_f32_16x16x4f32(xcur[ks], Rq[4 * ks * 32 + 16 * h], gx[0][h], 0, 0, 0);
+      const f32x4 r0 = gx[0][0], r1 = gx[0][1];
+#pragma unroll
+      for (int k = 0; k + 1 < NT; ++k) {
+        gx[k][0] = gx[k + 1][0];
+        gx[k][1] = gx[k + 1][1];
+      }
+      gx[NT - 1][0] = r0;
+      gx[NT - 1][1] = r1;
+      ++gxs;
+    };
+    if constexpr (GX) {
+#pragma unroll
+      for (int k = 0; k < NT; ++k) gx[k][0] = gx[k][1] = f32x4{};
+      load_gx_x(1, xnext);
+    }
     for (int t = 1; t <= T; ++t) {
       const __bf16* A = &Ab[t & 1][c * AST + 8 * kh];
 #pragma unroll 1
@@ -374,6 +427,10 @@ __global__ __launch_bounds__(SR_THREADS) void k_sweep_rows(Geom g, const bf16x8*
 #pragma unroll
           for (int p = 0; p < 3; ++p) bq[u][p] = wq[(Gn * 3 + p) * 64];
           if (cc == KC2 - 1) {
+            // GX: the slot still holds R of tile s - 2 (the consumer's, one step ago): fold it in
+            // before this tile's z overwrites it (same wave, LDS ops in order)
+            if constexpr (GX)
+              if ((t - 1) * NT + n >= 2) gx_fold(((t - 1) * NT + n) & 1);
             float* Z = &Zb[((t - 1) * NT + n) & 1][q * SR_ROWS * 32 + c];
 #pragma unroll
             for (int r = 0; r < 16; ++r) Z[acc_row(r, lane) * 32] = acc[r];
@@ -383,7 +440,24 @@ __global__ __launch_bounds__(SR_THREADS) void k_sweep_rows(Geom g, const bf16x8*
         }
       }
     }
+    const int slast = T * NT - 1;
+    if constexpr (GX)
+      if (slast >= 1) gx_fold((slast - 1) & 1);   // R of tile slast - 1 (consumer's step slast)
     __syncthreads();         // final step: the consumer drains the last tile
+    if constexpr (GX) {
+      gx_fold(slast & 1);
+      // slot k = column tile k; C map of 16x16x4: row d = 4 (lane / 16) + v, column lane % 16
+      float* out = a.gx_slab + ((int64_t)blockIdx.x * 4 + q) * D * H;
+#pragma unroll
+      for (int k = 0; k < NT; ++k)
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+          for (int v = 0; v < 4; ++v) {
+            const int d = 4 * (lane >> 4) + v;
+            if (d < D) out[(int64_t)d * H + 32 * k + 16 * h + (lane & 15)] = gx[k][h][v];
+          }
+    }
 #ifdef SR_TIMING
     if (threadIdx.x == 0) { g_sr_wait[blockIdx.x][0] = sr_wait; g_sr_wait[blockIdx.x][1] = clock64() - sr_t0; }
 #endif
@@ -462,9 +536,10 @@ __global__ __launch_bounds__(SR_THREADS) void k_sweep_rows(Geom g, const bf16x8*
 #endif
       if (n + 1 < NT) load_tile(t, n + 1, nxt);
       else if (!last) load_tile(t + 1, 0, nxt);
-      const f32x4* Z = reinterpret_cast<const f32x4*>(&Zb[((t - 1) * NT + n) & 1][row * 32 + j4]);
+      f32x4* Z = reinterpret_cast<f32x4*>(&Zb[((t - 1) * NT + n) & 1][row * 32 + j4]);
       const f32x4 zi = Z[0], zf = Z[SR_ROWS * 8], zg = Z[2 * SR_ROWS * 8], zo = Z[3 * SR_ROWS * 8];
       f32x4 i1, f1, g1, o1, c1, h1, li, lf, lg, lo, lc;
+      f32x4 ai, af, ag, ao, di, df, dg, dO;   // phi(z), phi'(z) (GX)
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
         SweepIn v;
@@ -474,6 +549,18 @@ __global__ __launch_bounds__(SR_THREADS) void k_sweep_rows(Geom g, const bf16x8*
         const SweepRes o = sweep_point(hp, v, last);
         i1[u] = o.i1; f1[u] = o.f1; g1[u] = o.g1; o1[u] = o.o1; c1[u] = o.c1; h1[u] = o.h1;
         li[u] = o.li; lf[u] = o.lf; lg[u] = o.lg; lo[u] = o.lo; lc[u] = o.lc;
+        ai[u] = o.ai; af[u] = o.af; ag[u] = o.ag; ao[u] = o.ao;
+        di[u] = o.di; df[u] = o.df; dg[u] = o.dg; dO[u] = o.dO;
+      }
+      // lam/rho + S of the updated i, f, g, o: the next x stage's targets (tgt_quot, as k_resid_gx)
+      const f32x4 ti = tgt_quot(li, hp.rho[0], i1), tf = tgt_quot(lf, hp.rho[1], f1);
+      const f32x4 tg = tgt_quot(lg, hp.rho[2], g1), to = tgt_quot(lo, hp.rho[3], o1);
+      if constexpr (GX) {   // R = (phi(z) - tgt) phi'(z) into the z slot (0 past the last row)
+        const float m = rok ? 1.f : 0.f;
+        Z[0] = (ai - ti) * di * m;
+        Z[SR_ROWS * 8] = (af - tf) * df * m;
+        Z[2 * SR_ROWS * 8] = (ag - tg) * dg * m;
+        Z[3 * SR_ROWS * 8] = (ao - to) * dO * m;
       }
 #ifdef SR_TIMING
       asm volatile("" :: "v"(i1), "v"(f1), "v"(g1), "v"(o1), "v"(c1), "v"(h1), "v"(li), "v"(lf), "v"(lg), "v"(lo), "v"(lc));
@@ -500,8 +587,8 @@ __global__ __launch_bounds__(SR_THREADS) void k_sweep_rows(Geom g, const bf16x8*
         buf_st4s(rZ, zo4, 3 * zpl, zo);
       }
       if (wtgt && rok) {   // same expression as k_resid_gx (tgt_quot), so either source gives equal bits
-        buf_st4s(rT, zo4, 0, tgt_quot(li, hp.rho[0], i1)); buf_st4s(rT, zo4, zpl, tgt_quot(lf, hp.rho[1], f1));
-        buf_st4s(rT, zo4, 2 * zpl, tgt_quot(lg, hp.rho[2], g1)); buf_st4s(rT, zo4, 3 * zpl, tgt_quot(lo, hp.rho[3], o1));
+        buf_st4s(rT, zo4, 0, ti); buf_st4s(rT, zo4, zpl, tf);
+        buf_st4s(rT, zo4, 2 * zpl, tg); buf_st4s(rT, zo4, 3 * zpl, to);
       }
 #ifdef SR_TIMING
       const unsigned long long tc_ = clock64();
@@ -2082,7 +2169,10 @@ template <int XC>
 static void launch_sweep_rows_xc(const Geom& g, const bf16x8* wt, const Hyper& hp, const SweepT& a, hipStream_t s) {
   dim3 grid(cdiv64(a.r1 - a.r0, SR_ROWS));
   switch (g.H / 32) {
-#define SR_CASE(N) case N: k_sweep_rows<N, XC><<<grid, SR_THREADS, 0, s>>>(g, wt, hp, a); break;
+#define SR_CASE(N) case N: \
+  if (XC == 1 && a.gx_slab) k_sweep_rows<N, XC, true><<<grid, SR_THREADS, 0, s>>>(g, wt, hp, a); \
+  else k_sweep_rows<N, XC, false><<<grid, SR_THREADS, 0, s>>>(g, wt, hp, a); \
+  break;
     SR_CASE(2) SR_CASE(3) SR_CASE(4) SR_CASE(5) SR_CASE(6) SR_CASE(7) SR_CASE(8)
 #undef SR_CASE
     default: break;

@@ -89,6 +89,7 @@ struct SweepT {
   Planes6 S, L;             // [B,T+1,H] each
   float* zc;                // [4][B*T][H]: z cache for the next step's first weight stage
   float* tgt;               // [4][B*T][H]: lam/rho + S of the updated state (k_sweep_rows; nullable)
+  float* gx_slab;           // [blocks][4][D][H]: next x stage's X^T R partials (k_sweep_rows, D <= 16; nullable)
   int64_t r0, r1;           // sample rows [r0, r1) of this launch
 };
 void launch_sweep_t(const Geom& g, int t, const Weights& w, const Hyper& hp, const SweepT& a, hipStream_t s);

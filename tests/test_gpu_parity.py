@@ -667,6 +667,42 @@ def test_speculative_x_update_bit_identical(shape, D_, mods, dev, monkeypatch):
     assert torch.equal(out[0][2], out[1][2])
 
 
+@pytest.mark.parametrize('shape,D_', [((300, 3, 256), 16), ((200, 5, 64), 5), ((8192, 8, 256), 16)])
+def test_sweep_gx_matches_resid_pass(shape, D_, mods, dev, monkeypatch):
+    """k_sweep_rows<GX> forms the next x stage's X^T R partials with f32 MFMAs from the new
+    state (default); ADMM_GX_SWEEP=0 runs k_resid_gx over z and tgt instead.  Same products,
+    another summation order: identical line-search exponents, weights and state within fp32
+    rounding (1e-5), over several steps.  B % 32 != 0 covers the ragged last row block."""
+    from blocks.lstm import LSTM
+    from parameters import example_parameter_dictionary
+    admm, _ = mods
+    admm.with_dual_y = False
+    B, T, H = shape
+    g = torch.Generator().manual_seed(17)
+    x = torch.rand(B, T, D_, generator=g).to(dev)
+    y = (0.8 * x.mean((1, 2)).unsqueeze(1) + 0.1 * torch.rand(B, 1, generator=g).to(dev)).contiguous()
+    out = []
+    for mode in ('0', '1'):
+        monkeypatch.setenv('ADMM_GX_SWEEP', mode)
+        torch.manual_seed(0)
+        m = LSTM(D_, H, 1).to(dev)
+        opt = admm.ADMMBasedOptimizer(m, (x, y), example_parameter_dictionary['GoogleStock'], verbose=False)
+        ks = []
+        for _ in range(4):
+            opt.step()
+            ks.append(list(opt.last_step_stats()['k'].values()))
+        out.append((ks, {n: p.detach().clone() for n, p in m.named_parameters()},
+                    {q: opt.gates[q].clone() for q in GATES6}, _loss(m, x, y)))
+        del opt
+    assert out[0][0] == out[1][0]
+    for n in out[0][1]:
+        a, b = out[1][1][n], out[0][1][n]
+        assert float((a - b).abs().max()) <= 1e-5 * max(1.0, float(b.abs().max())), n
+    for q in GATES6:
+        assert float((out[1][2][q] - out[0][2][q]).abs().max()) <= 1e-5, q
+    assert out[1][3] == pytest.approx(out[0][3], rel=1e-5)
+
+
 def test_generic_weight_stage_matches_fast(mods, dev, monkeypatch):
     """ADMM_GENERIC=1 runs the weight stages on the generic kernels (materialised R and Q, f32 MFMA
     GEMMs) instead of the fast streaming path.  Step 1 decides identically on both: the x-side

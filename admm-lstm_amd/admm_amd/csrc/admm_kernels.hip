@@ -409,6 +409,7 @@ __global__ __launch_bounds__(SR_THREADS) void k_sweep_rows(Geom g, const bf16x8*
       const __bf16* A = &Ab[t & 1][c * AST + 8 * kh];
 #pragma unroll 1
       for (int G0 = 0; G0 < GT; G0 += U) {
+        int ended = -1;   // GX: the tile step that ended in this group (at most one: KC2 > U)
 #pragma unroll
         for (int u = 0; u < U; ++u) {
           const int G = G0 + u, n = G / KC2, cc = G - n * KC2;
@@ -427,22 +428,26 @@ __global__ __launch_bounds__(SR_THREADS) void k_sweep_rows(Geom g, const bf16x8*
 #pragma unroll
           for (int p = 0; p < 3; ++p) bq[u][p] = wq[(Gn * 3 + p) * 64];
           if (cc == KC2 - 1) {
-            // GX: the slot still holds R of tile s - 2 (the consumer's, one step ago): fold it in
-            // before this tile's z overwrites it (same wave, LDS ops in order)
-            if constexpr (GX)
-              if ((t - 1) * NT + n >= 2) gx_fold(((t - 1) * NT + n) & 1);
             float* Z = &Zb[((t - 1) * NT + n) & 1][q * SR_ROWS * 32 + c];
 #pragma unroll
             for (int r = 0; r < 16; ++r) Z[acc_row(r, lane) * 32] = acc[r];
             acc = f32x16{};
-            SR_SYNC();   // end of step
+            if constexpr (GX) ended = (t - 1) * NT + n;
+            else SR_SYNC();   // end of step
           }
         }
+        // GX: the end-of-step barrier moves to the group's end (the next tile's chunks of this
+        // group read only A and B), so that the fold below exists once, not in every unrolled
+        // slot.  Past the barrier of step s the consumer's R of tile s - 1 is in its slot, which
+        // the z of tile s + 1 overwrites only at that tile's end.
+        if constexpr (GX)
+          if (ended >= 0) {
+            SR_SYNC();   // end of step
+            if (ended >= 1) gx_fold((ended - 1) & 1);
+          }
       }
     }
     const int slast = T * NT - 1;
-    if constexpr (GX)
-      if (slast >= 1) gx_fold((slast - 1) & 1);   // R of tile slast - 1 (consumer's step slast)
     __syncthreads();         // final step: the consumer drains the last tile
     if constexpr (GX) {
       gx_fold(slast & 1);

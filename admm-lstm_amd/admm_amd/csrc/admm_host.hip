@@ -93,6 +93,11 @@ struct AdmmCtx {
   // ... and the next x stage's X^T R partials (k_sweep_rows GX, D <= 16), so that stage skips
   // k_resid_gx (ADMM_GX_SWEEP=0 disables)
   bool gx_sweep = true;
+  // dual h before T: zero unless written from outside (the library ascends it only at T);
+  // lamh_known says whether lamh_nz (device) describes the bound plane
+  int* lamh_nz = nullptr;
+  bool lamh_known = false;
+  bool lamh_skip = true;   // ADMM_LAMH_SKIP=0: always load it
   bool gx_valid = false;
   float* gx_slab = nullptr;   // [sweep blocks][4][D][H]
   int gx_nblk = 0;
@@ -348,6 +353,12 @@ int stage_sweep(AdmmCtx* c, hipStream_t s) {
     sa.r1 = g.B;
     sa.tgt = fast_path(g) && c->tgt_sweep ? c->tgt : nullptr;   // the fast x stage reads it next step
     sa.gx_slab = sa.tgt ? c->gx_slab : nullptr;
+    if (g.H % 4 == 0 && g.T > 1 && !c->lamh_known) {
+      HIP_TRY(hipMemsetAsync(c->lamh_nz, 0, sizeof(int), s));
+      launch_check_lamh(g, c->buf.duals[ADMM_H], c->lamh_nz, s);
+      c->lamh_known = true;
+    }
+    sa.lamh_nz = c->lamh_known && c->lamh_skip ? c->lamh_nz : nullptr;
     launch_sweep_wt(g, w, c->swt, s);
     launch_sweep_rows(g, c->swt, c->hp, sa, s);
   } else {
@@ -438,6 +449,7 @@ int admm_create(const AdmmDims* dims, const AdmmParams* params, int device, Admm
   if (const char* e = std::getenv("ADMM_SWEEP_ROWS")) c->sweep_rows = c->sweep_rows && std::atoi(e) != 0;
   if (const char* e = std::getenv("ADMM_TGT_SWEEP")) c->tgt_sweep = std::atoi(e) != 0;
   if (const char* e = std::getenv("ADMM_GX_SWEEP")) c->gx_sweep = std::atoi(e) != 0;
+  if (const char* e = std::getenv("ADMM_LAMH_SKIP")) c->lamh_skip = std::atoi(e) != 0;
   if (const char* e = std::getenv("ADMM_GENERIC")) c->force_generic = std::atoi(e) != 0;
   c->split3 = fast_path(g) && split3_ok(g);
   c->spec_x = fast_path(g) && trial_rows_ok(g);
@@ -475,7 +487,7 @@ int admm_create(const AdmmDims* dims, const AdmmParams* params, int device, Admm
       (rc = dalloc(&c->found, 4)) || (rc = dalloc(&c->pick, 4)) ||
       (rc = dalloc(&c->U, (size_t)g.B * g.O)) || (rc = dalloc(&c->wy_slab, (size_t)c->wy_nsplit * g.H * g.O)) ||
       (rc = dalloc(&c->Gy, (size_t)g.H * g.O)) || (rc = dalloc(&c->ht_part, (size_t)c->ht_nblk * kHTSums)) ||
-      (rc = dalloc(&c->ht_sums, kHTSums)) || (rc = dalloc(&c->stats, 1)) ||
+      (rc = dalloc(&c->ht_sums, kHTSums)) || (rc = dalloc(&c->stats, 1)) || (rc = dalloc(&c->lamh_nz, 1)) ||
       (c->sweep_rows && (rc = dalloc(&c->swt, sweep_wt_floats(g)))) ||
       (c->split3 && (rc = dalloc(&c->gimg, split3_gimg_floats(g)))) ||
       (c->spec_x && ((rc = dalloc(&c->zx, 4 * plane)) || (rc = dalloc(&c->kpred, 4)))) ||
@@ -510,7 +522,7 @@ int admm_destroy(AdmmCtx* c) {
   if (!c) return ADMM_OK;
   DeviceGuard dg_(c->device);
   void* ptrs[] = {c->zc, c->tgt, c->R, c->Q, c->G, c->dW, c->gslab, c->tr_part, c->tr_sums, c->tr_poly, c->found, c->pick,
-                  c->U, c->wy_slab, c->Gy, c->ht_part, c->ht_sums, c->stats, c->swt, c->gimg, c->zx, c->kpred, c->gx_slab};
+                  c->U, c->wy_slab, c->Gy, c->ht_part, c->ht_sums, c->stats, c->swt, c->gimg, c->zx, c->kpred, c->gx_slab, c->lamh_nz};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   if (c->comm) ncclCommDestroy(c->comm);
@@ -543,6 +555,7 @@ int admm_bind(AdmmCtx* c, const AdmmBuffers* b) {
   c->z_valid = false;
   c->tgt_valid = false;
   c->gx_valid = false;
+  c->lamh_known = false;
   return ADMM_OK;
 }
 
@@ -557,6 +570,7 @@ int admm_invalidate_cache(AdmmCtx* c) {
   c->z_valid = false;
   c->tgt_valid = false;
   c->gx_valid = false;
+  c->lamh_known = false;
   return ADMM_OK;
 }
 
@@ -595,6 +609,8 @@ int admm_init_state(AdmmCtx* c, void* stream) {
   c->z_valid = true;
   c->tgt_valid = false;   // recomputed from the new state by the first x stage
   c->gx_valid = false;
+  HIP_TRY(hipMemsetAsync(c->lamh_nz, 0, sizeof(int), s));   // the duals were just zeroed
+  c->lamh_known = true;
   return ADMM_OK;
 }
 

@@ -495,15 +495,19 @@ __global__ __launch_bounds__(SR_THREADS) void k_sweep_rows(Geom g, const bf16x8*
   const uint32_t pofs = (uint32_t)(((m0 + row) * rs + j4) * 4);       // t = 0, tile 0
   const uint32_t zofs = (uint32_t)(((m0 + row) * T * H + j4) * 4);    // t = 1, tile 0
 
+  // The dual of h is zero before T (admm.py:504-539 ascends it only at t = T) unless the caller
+  // wrote it: a.lamh_nz, set by k_check_lamh after every external change, says which.
+  const bool lh_zero = a.lamh_nz != nullptr && *a.lamh_nz == 0;
   struct St4 { f32x4 f0, g0, c0, h0, cp, li, lf, lg, lo, lc, lh; };
   auto load_tile = [&](int t, int n, St4& v) {
     const uint32_t o = pofs + (uint32_t)(t * H + 32 * n) * 4;
     v.f0 = buf_ld4(rS[1], o); v.g0 = buf_ld4(rS[2], o); v.c0 = buf_ld4(rS[4], o); v.h0 = buf_ld4(rS[5], o);
-    // c_{t-1}, stored by this thread one t earlier: read past the CU's vector L1 (sc0 sc1; a
-    // cached load may return the line as it was before that store -- nondeterministic sweeps)
-    v.cp = buf_ld4<kAuxL2>(rS[4], o - H * 4);
+    // c_{t-1}: from the state plane only at t = 1 (the initial c); later this thread's own
+    // update of the previous t, kept in registers (cring)
+    if (t == 1) v.cp = buf_ld4(rS[4], o - H * 4);
     v.li = buf_ld4(rL[0], o); v.lf = buf_ld4(rL[1], o); v.lg = buf_ld4(rL[2], o);
-    v.lo = buf_ld4(rL[3], o); v.lc = buf_ld4(rL[4], o); v.lh = buf_ld4(rL[5], o);
+    v.lo = buf_ld4(rL[3], o); v.lc = buf_ld4(rL[4], o);
+    v.lh = lh_zero && t < T ? f32x4{} : buf_ld4(rL[5], o);
   };
   // x_{tn} into A-buffer tn&1 (32 rows x XK)
   auto load_x = [&](int tn) {
@@ -516,9 +520,12 @@ __global__ __launch_bounds__(SR_THREADS) void k_sweep_rows(Geom g, const bf16x8*
     }
   };
 
-  // Tile operands are loaded one tile early.  A tile's c_{t-1} is stored NT tiles before its own
-  // step, so the read-back needs NT > 1 (loading two tiles ahead measured no faster).
-  static_assert(NT > 1, "c_{t-1} read-back needs the store NT tiles earlier");
+  // Tile operands are loaded one tile early (loading two tiles ahead measured no faster).
+  // cring[0] is c_{t-1} of the tile being updated: popped at every tile, c_t pushed at the back.
+  static_assert(NT > 1, "the mid-step barrier protocol needs two or more column tiles");
+  f32x4 cring[NT];
+#pragma unroll
+  for (int k = 0; k < NT; ++k) cring[k] = f32x4{};
   St4 nxt;
   load_tile(1, 0, nxt);
   load_x(2);                 // step 0: the producer computes tile (1, 0)
@@ -545,11 +552,12 @@ __global__ __launch_bounds__(SR_THREADS) void k_sweep_rows(Geom g, const bf16x8*
       const f32x4 zi = Z[0], zf = Z[SR_ROWS * 8], zg = Z[2 * SR_ROWS * 8], zo = Z[3 * SR_ROWS * 8];
       f32x4 i1, f1, g1, o1, c1, h1, li, lf, lg, lo, lc;
       f32x4 ai, af, ag, ao, di, df, dg, dO;   // phi(z), phi'(z) (GX)
+      const f32x4 cpv = t == 1 ? cur.cp : cring[0];
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
         SweepIn v;
         v.zi = zi[u]; v.zf = zf[u]; v.zg = zg[u]; v.zo = zo[u];
-        v.f0 = cur.f0[u]; v.g0 = cur.g0[u]; v.c0 = cur.c0[u]; v.h0 = cur.h0[u]; v.cp = cur.cp[u];
+        v.f0 = cur.f0[u]; v.g0 = cur.g0[u]; v.c0 = cur.c0[u]; v.h0 = cur.h0[u]; v.cp = cpv[u];
         v.li = cur.li[u]; v.lf = cur.lf[u]; v.lg = cur.lg[u]; v.lo = cur.lo[u]; v.lc = cur.lc[u]; v.lh = cur.lh[u];
         const SweepRes o = sweep_point(hp, v, last);
         i1[u] = o.i1; f1[u] = o.f1; g1[u] = o.g1; o1[u] = o.o1; c1[u] = o.c1; h1[u] = o.h1;
@@ -557,6 +565,9 @@ __global__ __launch_bounds__(SR_THREADS) void k_sweep_rows(Geom g, const bf16x8*
         ai[u] = o.ai; af[u] = o.af; ag[u] = o.ag; ao[u] = o.ao;
         di[u] = o.di; df[u] = o.df; dg[u] = o.dg; dO[u] = o.dO;
       }
+#pragma unroll
+      for (int k = 0; k + 1 < NT; ++k) cring[k] = cring[k + 1];
+      cring[NT - 1] = c1;
       // lam/rho + S of the updated i, f, g, o: the next x stage's targets (tgt_quot, as k_resid_gx)
       const f32x4 ti = tgt_quot(li, hp.rho[0], i1), tf = tgt_quot(lf, hp.rho[1], f1);
       const f32x4 tg = tgt_quot(lg, hp.rho[2], g1), to = tgt_quot(lo, hp.rho[3], o1);
@@ -581,7 +592,7 @@ __global__ __launch_bounds__(SR_THREADS) void k_sweep_rows(Geom g, const bf16x8*
       }
       const uint32_t po = pofs + (uint32_t)(t * H + 32 * n) * 4, zo4 = zofs + (uint32_t)((t - 1) * H + 32 * n) * 4;
       buf_st4(rS[0], po, i1); buf_st4(rS[1], po, f1); buf_st4(rS[2], po, g1); buf_st4(rS[3], po, o1);
-      buf_st4<0>(rS[4], po, c1);             // c_t: read back at t+1 (here) and by the next step's kernels
+      buf_st4<0>(rS[4], po, c1);             // c_t: read by the next step's kernels
       if (!last) buf_st4<0>(rS[5], po, h1);
       buf_st4(rL[0], po, li); buf_st4(rL[1], po, lf); buf_st4(rL[2], po, lg); buf_st4(rL[3], po, lo);
       buf_st4(rL[4], po, lc);
@@ -2134,7 +2145,25 @@ __global__ __launch_bounds__(kThreads) void k_ht_apply(Geom g, Hyper hp, Planes6
 
 }  // namespace
 
+// flag <- 1 if the dual of h has a nonzero entry at some t in [1, T) (k_sweep_rows lh_zero)
+__global__ __launch_bounds__(kThreads) void k_check_lamh(Geom g, const float* __restrict__ lh, int* flag) {
+  const int64_t H4 = g.H / 4, per_b = (int64_t)(g.T - 1) * H4, n = g.B * per_b;
+  bool nz = false;
+  for (int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x; i < n; i += (int64_t)gridDim.x * kThreads) {
+    const int64_t b = i / per_b, r = i - b * per_b;
+    const float4 v = ld_nt(lh + b * g.TP() * g.H + g.H + 4 * r);
+    nz |= (v.x != 0.f) | (v.y != 0.f) | (v.z != 0.f) | (v.w != 0.f);
+  }
+  if (__any(nz) && (threadIdx.x & 63) == 0) atomicOr(flag, 1);
+}
+
 // ============================================================================ launchers
+
+void launch_check_lamh(const Geom& g, const float* lh, int* flag, hipStream_t s) {
+  const int64_t n = g.B * (int64_t)(g.T - 1) * (g.H / 4);
+  const int nb = (int)std::max<int64_t>(1, std::min<int64_t>(cdiv64(n, kThreads), 2048));
+  k_check_lamh<<<nb, kThreads, 0, s>>>(g, lh, flag);
+}
 
 // float4 staging needs 16-byte aligned rows of x and of the [.., H] planes
 inline int vec_ok(const Geom& g) { return (g.D % 4 == 0 && g.H % 4 == 0) ? 1 : 0; }

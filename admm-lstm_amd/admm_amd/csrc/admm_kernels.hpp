@@ -90,6 +90,7 @@ struct SweepT {
   float* zc;                // [4][B*T][H]: z cache for the next step's first weight stage
   float* tgt;               // [4][B*T][H]: lam/rho + S of the updated state (k_sweep_rows; nullable)
   float* gx_slab;           // [blocks][4][D][H]: next x stage's X^T R partials (k_sweep_rows, D <= 16; nullable)
+  const int* lamh_nz;       // k_sweep_rows: device flag, 0 = dual h is zero at every t < T (nullable: unknown)
   int64_t r0, r1;           // sample rows [r0, r1) of this launch
 };
 void launch_sweep_t(const Geom& g, int t, const Weights& w, const Hyper& hp, const SweepT& a, hipStream_t s);
@@ -99,6 +100,8 @@ bool sweep_rows_ok(const Geom& g);
 size_t sweep_wt_floats(const Geom& g);
 void launch_sweep_wt(const Geom& g, const Weights& w, float* wt, hipStream_t s);
 void launch_sweep_rows(const Geom& g, const float* wt, const Hyper& hp, const SweepT& a, hipStream_t s);
+// flag |= 1 if lh[b][t][j] != 0 for some t in [1, T) (H % 4 == 0; flag zeroed by the caller)
+void launch_check_lamh(const Geom& g, const float* lh, int* flag, hipStream_t s);
 
 
 // out[b][o] = h_row(b) . wy[:, o]

@@ -74,9 +74,19 @@ def roofline_terms(cls: str, B: int, T: int, D: int, H: int):
     f4 = 4  # bytes per fp32
     tgt = tgt_from_sweep(H)
     if cls == 'sweep':            # whole sweep t = 1..T: per t [B, D+H] x [D+H, 4H] + fused gate/dual updates
-        # per (b, t, j): 11 state/dual loads (incl. c_{t-1}), 15 stores (6 gates, 5 duals, 4 z),
-        # + 4 tgt stores when the sweep writes the next x stage's targets
-        return T * 2.0 * B * (D + H) * 4 * H, T * f4 * B * (D + (30 if tgt else 26) * H)
+        flops = T * 2.0 * B * (D + H) * 4 * H
+        if not tgt:               # per-t sweep: 11 state/dual loads (incl. c_{t-1}), 15 stores (6 gates, 5 duals, 4 z)
+            return flops, T * f4 * B * (D + 26 * H)
+        # persistent sweep, per (b, t, j): 9 state/dual loads (f, g, c, h; duals of i, f, g, o, c),
+        # 19 stores (6 gates, 5 duals, 4 z, 4 tgt).  c_{t-1} comes from registers after t = 1 and
+        # the h dual is read only at T while it is zero before T (the reference's invariant):
+        # one plane slice each, once.  With D <= 16 the sweep also forms the next x stage's
+        # X^T R partials: x once more, and a [blocks][4][D][H] slab.
+        lamh_all = os.environ.get('ADMM_LAMH_SKIP', '1') == '0'
+        byts = T * f4 * B * (D + (29 if lamh_all else 28) * H) + f4 * B * (1 if lamh_all else 2) * H
+        if D <= 16 and os.environ.get('ADMM_GX_SWEEP', '1') != '0':
+            byts += f4 * B * T * D + f4 * ((B + 31) // 32) * 4 * D * H
+        return flops, byts
     n = float(B) * T * H          # elements of one [B*T, H] plane
     if cls == 'atr_h':            # G_q = Hprev^T R_q, 4 gates
         return 2.0 * B * T * H * 4 * H, f4 * (B * T * H + 4 * n)
@@ -90,6 +100,8 @@ def roofline_terms(cls: str, B: int, T: int, D: int, H: int):
         return 0.0, f4 * 3 * 4 * n
     if cls == 'resid':            # x-stage residual (read z and tgt, or z, lam, S and write tgt) + z += X dWx
         return 0.0, f4 * ((2 if tgt else 4) + 2) * 4 * n
+    # trials: pass 0 of the x side reads z and tgt and (H % 256 == 0) writes z + x dWx for the
+    # predicted exponent; the h side reads z, tgt and Q -- three planes per gate either way
     return None
 
 

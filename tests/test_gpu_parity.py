@@ -373,7 +373,7 @@ def test_external_weight_change_invalidates_cache(mods, dev):
         assert torch.equal(p.detach(), got[n]), n
 
 
-@pytest.mark.parametrize('edit', ["duals['i']", "gates['o']", "duals['c']"])
+@pytest.mark.parametrize('edit', ["duals['i']", "gates['o']", "duals['c']", "duals['h']"])
 def test_inplace_state_edit_invalidates_targets(edit, mods, dev):
     """The persistent sweep leaves the x stage's targets tgt = dual/rho + gate in the
     library (DESIGN.md "tgt from the sweep").  Editing a gate or dual plane in place
@@ -476,9 +476,13 @@ def test_full_size_c3_properties(mods, dev):
     assert l1[3] < l1[0]
 
 
-def test_persistent_sweep_matches_per_t_sweep(mods, dev, monkeypatch):
+@pytest.mark.parametrize('lamh_edit', [False, True])
+def test_persistent_sweep_matches_per_t_sweep(lamh_edit, mods, dev, monkeypatch):
     """The two sweep implementations (one persistent launch vs one launch per t, chosen at
-    create time by ADMM_SWEEP_ROWS) agree on a C3-shaped step (H = 256, D = 16)."""
+    create time by ADMM_SWEEP_ROWS) agree on a C3-shaped step (H = 256, D = 16).  The
+    persistent sweep skips the loads of the h dual before T while it is known to be zero (the
+    reference ascends it only at T); lamh_edit writes nonzero values there between the steps,
+    which the per-t sweep always reads: the persistent sweep must notice and read them too."""
     from blocks.lstm import LSTM
     from parameters import example_parameter_dictionary
     admm, _ = mods
@@ -494,13 +498,54 @@ def test_persistent_sweep_matches_per_t_sweep(mods, dev, monkeypatch):
         torch.manual_seed(0)
         m = LSTM(D, H, 1).to(dev)
         opt = admm.ADMMBasedOptimizer(m, (x, y), pd, verbose=False)
-        for _ in range(2):
+        for i in range(2):
             opt.step()
+            if lamh_edit and i == 0:
+                gen = torch.Generator().manual_seed(5)
+                with torch.no_grad():
+                    opt.duals['h'][:, 1:T].add_(0.01 * torch.rand(B, T - 1, H, generator=gen).to(dev))
         out[flag] = ({q: opt.gates[q].clone() for q in GATES6}, {q: opt.duals[q].clone() for q in GATES6})
     for k in (0, 1):
         for q in GATES6:
             d = float((out['1'][k][q] - out['0'][k][q]).abs().max())
-            assert d <= 1e-5, (k, q, d)
+            # the edited dual drives h (and then c) far from [-1, 1] (h = -lam_h / rho_h) and the
+            # pre-activations with it: relative, and the two GEMMs' (f32 vs split bf16) rounding
+            # grows with them (the skip itself is checked bit for bit below)
+            scale = 5 * max(1.0, float(out['0'][k][q].abs().max())) if lamh_edit else 1.0
+            assert d <= 1e-5 * scale, (k, q, d, scale)
+
+
+@pytest.mark.parametrize('lamh_edit', [False, True])
+def test_lamh_skip_bit_identical(lamh_edit, mods, dev, monkeypatch):
+    """The persistent sweep's skip of the h dual's loads before T (zero there unless written from
+    outside, checked by k_check_lamh after every external change) against ADMM_LAMH_SKIP=0
+    (always loaded): bit-identical, with the reference's zero plane and with nonzero values
+    written between steps."""
+    from blocks.lstm import LSTM
+    from parameters import example_parameter_dictionary
+    admm, _ = mods
+    admm.with_dual_y = False
+    B, T, D, H = 300, 4, 16, 256
+    g = torch.Generator().manual_seed(11)
+    x = torch.rand(B, T, D, generator=g).to(dev)
+    y = torch.rand(B, 1, generator=g).to(dev)
+    out = []
+    for flag in ('1', '0'):
+        monkeypatch.setenv('ADMM_LAMH_SKIP', flag)
+        torch.manual_seed(0)
+        m = LSTM(D, H, 1).to(dev)
+        opt = admm.ADMMBasedOptimizer(m, (x, y), example_parameter_dictionary['GoogleStock'], verbose=False)
+        for i in range(3):
+            opt.step()
+            if lamh_edit and i == 0:
+                gen = torch.Generator().manual_seed(5)
+                with torch.no_grad():
+                    opt.duals['h'][:, 1:T].add_(0.01 * torch.rand(B, T - 1, H, generator=gen).to(dev))
+        out.append(torch.cat([p.detach().flatten() for p in m.parameters()]
+                             + [v.flatten() for v in opt.gates.values()] + [v.flatten() for v in opt.duals.values()]))
+        del opt
+    assert torch.isfinite(out[0]).all()
+    assert torch.equal(out[0], out[1])
 
 
 def test_split3_h_stage_matches_f32_mfma(mods, dev, monkeypatch):

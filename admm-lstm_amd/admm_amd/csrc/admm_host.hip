@@ -312,7 +312,8 @@ int stage_weights(AdmmCtx* c, int side, hipStream_t s) {
   sa.stats = c->stats;
   const int nblk = fast ? stream_blocks(g) : c->nblk_trial;
   // the row-pair trial kernel (H % 256 == 0) writes one partial per (block, column block)
-  const int nred = fast && trial_rows_ok(g) ? nblk * (g.H / 256) : nblk;
+  const int nred = fast && side == 0 && trial_mx_ok(g) ? nblk * (g.H / 128)
+                   : fast && trial_rows_ok(g) ? nblk * (g.H / 256) : nblk;
   for (int pass = 0; pass < kMaxPasses; ++pass) {
     {
       ProfScope ps(c, pass == 0 ? ADMM_PROF_TRIAL : ADMM_PROF_TRIAL_EXTRA, s);
@@ -470,7 +471,7 @@ int admm_create(const AdmmDims* dims, const AdmmParams* params, int device, Admm
   c->gx_nblk = c->sweep_rows && fast_path(g) && c->tgt_sweep && c->gx_sweep && g.D <= 16 ? (int)((g.B + 31) / 32) : 0;
   const int Kmax = g.D > g.H ? g.D : g.H;
   c->nblk_resid = resid_blocks(g);
-  c->nblk_trial = std::max(trial_blocks(g), stream_blocks(g) * (trial_rows_ok(g) ? g.H / 256 : 1));
+  c->nblk_trial = std::max(trial_blocks(g), stream_blocks(g) * (trial_mx_ok(g) ? g.H / 128 : trial_rows_ok(g) ? g.H / 256 : 1));
   c->nblk_rx = resid_gx_blocks(g);
   size_t slab = (size_t)atr_splits(g, 0) * 4 * g.D * g.H;
   slab = std::max(slab, (size_t)atr_splits(g, 1) * 4 * g.H * g.H);

@@ -1610,6 +1610,118 @@ __global__ __launch_bounds__(kThreads) void k_trial_rows(Geom g, int pass, const
   trial_block_store(acc, part, q, blockIdx.z * nblk + blk, nblk * gridDim.z);
 }
 
+// x-side trial pass on the matrix cores (H % 128 == 0, D <= 16): each wave owns a 32-column
+// block of one gate and walks 16-row tiles.  The trial direction q = X G_x (and with SPEC the
+// z update X dWx(kpred)) of a tile comes from v_mfma_f32_16x16x4_f32 chains over K = 16 (x
+// rows as the A operand, zero-padded past D; G_x / dWx columns as B, resident in VGPRs), and
+// the trial arithmetic (trial_pair) runs on the accumulator layout.  The wave's two 16x16
+// products take the even and the odd columns, so lane l holds columns 2 (l % 16) + {0, 1} of
+// rows 4 (l / 16) + v, v = 0..3: every z / tgt / zx access is a float2 per lane, 128 B per row,
+// and the two columns are trial_pair's packed halves.  This frees the VALU of the 32 FMAs per
+// element the row-pair kernel (k_trial_rows) spends on q and the z update.
+template <bool TANH, bool SPEC>
+__device__ __forceinline__ void trial_mx_body(const Geom& g, int q, int pass, const float* __restrict__ zc,
+                                              const float* __restrict__ tgt, const float* __restrict__ x,
+                                              const float* __restrict__ Gx, int blk, int nblk, float (&acc)[kSlots],
+                                              DirectQ& dq, const SpecX& sp) {
+  const int64_t BT = g.BT(), n = BT * g.H;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int col0 = (blockIdx.z * 4 + wave) * 32 + 2 * (lane & 15);   // this lane's column pair
+  const float* __restrict__ zq = zc + (int64_t)q * n + col0;
+  const float* __restrict__ tq = tgt + (int64_t)q * n + col0;
+  float* __restrict__ zxq = SPEC ? sp.zx + (int64_t)q * n + col0 : nullptr;
+  // B operands: row 4 s + lane/16 of G_x (and dWx) at column col0 + h (product h)
+  float gb[2][4], db[2][4];
+  const WUpd u = SPEC ? WUpd::make(sp.hp.rho[q], sp.hp.beta_x[q], g.T, sp.kpred[q]) : WUpd{};
+#pragma unroll
+  for (int s4 = 0; s4 < 4; ++s4) {
+    const int d = 4 * s4 + (lane >> 4);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      gb[h][s4] = d < g.D ? Gx[((int64_t)q * g.D + d) * g.H + col0 + h] : 0.f;
+      if constexpr (SPEC) {
+        const float w0 = d < g.D ? sp.W[q][(int64_t)d * g.H + col0 + h] : 0.f;
+        db[h][s4] = d < g.D ? u.apply(w0, gb[h][s4]) - w0 : 0.f;
+      }
+    }
+  }
+  f32x2 acc2[kPair];
+#pragma unroll
+  for (int k = 0; k < kPair; ++k) acc2[k] = f32x2{0.f, 0.f};
+  const int64_t ntile = (BT + 15) / 16;
+  // operands of one tile; the next tile's are loaded while this one is evaluated (rows past
+  // BT clamped: branch-free, masked by ok below)
+  struct In { float xa[4]; f32x2 zv[4], tv[4]; };
+  auto load = [&](int64_t tile, In& v) {
+    const int64_t row0 = tile * 16;
+    // A operand: x[row0 + lane % 16][4 s + lane / 16]
+    const int64_t xr = min(row0 + (lane & 15), BT - 1);
+#pragma unroll
+    for (int s4 = 0; s4 < 4; ++s4) {
+      const int d = 4 * s4 + (lane >> 4);
+      v.xa[s4] = d < g.D ? x[xr * g.D + d] : 0.f;
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int64_t row = min(row0 + 4 * (lane >> 4) + r, BT - 1);
+      v.zv[r] = __builtin_nontemporal_load(reinterpret_cast<const f32x2*>(zq + row * g.H));
+      v.tv[r] = __builtin_nontemporal_load(reinterpret_cast<const f32x2*>(tq + row * g.H));
+    }
+  };
+  In cur, nxt;
+  load(blk, cur);
+  for (int64_t tile = blk; tile < ntile; tile += nblk) {
+    const int64_t row0 = tile * 16;
+    load(tile + nblk < ntile ? tile + nblk : tile, nxt);
+    const float (&xa)[4] = cur.xa;
+    const f32x2 (&zv)[4] = cur.zv;
+    const f32x2 (&tv)[4] = cur.tv;
+    f32x4 qa[2] = {}, da[2] = {};
+#pragma unroll
+    for (int s4 = 0; s4 < 4; ++s4)
+#pragma unroll
+      for (int h = 0; h < 2; ++h) qa[h] = __builtin_amdgcn_mfma_f32_16x16x4f32(xa[s4], gb[h][s4], qa[h], 0, 0, 0);
+    if constexpr (SPEC) {
+#pragma unroll
+      for (int s4 = 0; s4 < 4; ++s4)
+#pragma unroll
+        for (int h = 0; h < 2; ++h) da[h] = __builtin_amdgcn_mfma_f32_16x16x4f32(xa[s4], db[h][s4], da[h], 0, 0, 0);
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        const int64_t row = row0 + 4 * (lane >> 4) + v;
+        if (row < BT)
+          __builtin_nontemporal_store(zv[v] + f32x2{da[0][v], da[1][v]}, reinterpret_cast<f32x2*>(zxq + row * g.H));
+      }
+    }
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {   // the two columns of row 4 (lane / 16) + v
+      const bool ok = row0 + 4 * (lane >> 4) + v < BT;
+      trial_pair<TANH>(ok, zv[v], tv[v], f32x2{qa[0][v], qa[1][v]}, pass, acc, acc2, dq, ok);
+      dq_run(dq, acc, false);
+    }
+    cur = nxt;
+  }
+  trial_pair_fold(acc, acc2);
+  dq_run(dq, acc, true);
+}
+
+template <bool SPEC>
+__global__ __launch_bounds__(kThreads, 3) void k_trial_mx(Geom g, int pass, const float* __restrict__ zc,
+                                                       const float* __restrict__ tgt, const float* __restrict__ x,
+                                                       const float* __restrict__ Gx, const int* __restrict__ found,
+                                                       double* __restrict__ part, int nblk, SpecX sp) {
+  const int q = blockIdx.y, blk = blockIdx.x;
+  if (found[q]) return;
+  float acc[kSlots];
+#pragma unroll
+  for (int k = 0; k < kSlots; ++k) acc[k] = 0.f;
+  __shared__ float dqbuf[kThreads / 64][5 * kDQ];
+  DirectQ dq{dqbuf[threadIdx.x >> 6], 0, 0};
+  if (q == 2) trial_mx_body<true, SPEC>(g, q, pass, zc, tgt, x, Gx, blk, nblk, acc, dq, sp);
+  else trial_mx_body<false, SPEC>(g, q, pass, zc, tgt, x, Gx, blk, nblk, acc, dq, sp);
+  trial_block_store(acc, part, q, blockIdx.z * nblk + blk, nblk * gridDim.z);
+}
+
 // After the x stage: zc += X dWx, so the h stage sees z = X Wx_new + Hprev Wh
 // (admm.py:298-300: the h-side search uses the already-updated x2q).
 // k_apply_fix (kpred != nullptr): zx = zc + X dWx, only for the gates whose decided x-side
@@ -2374,6 +2486,15 @@ void launch_apply_fix(const Geom& g, const float* x, const float* dW, const floa
 
 bool trial_rows_ok(const Geom& g) { return g.H % 256 == 0; }
 
+static int g_trial_mx = -1;
+bool trial_mx_ok(const Geom& g) {   // ADMM_TRIAL_MX=0: the x side on k_trial_rows (VALU q)
+  if (g_trial_mx < 0) {
+    const char* e = std::getenv("ADMM_TRIAL_MX");
+    g_trial_mx = e ? std::atoi(e) != 0 : 1;
+  }
+  return g_trial_mx && g.H % 256 == 0 && g.D <= 16;
+}
+
 void launch_trial_fast(const Geom& g, int side, int pass, const float* zc, const float* tgt, const float* Q,
                        const float* x, const float* Wsrc, const int* found, double* part, int nblk, hipStream_t s,
                        const SpecX* spec) {
@@ -2386,6 +2507,12 @@ void launch_trial_fast(const Geom& g, int side, int pass, const float* zc, const
   }
   if (side == 1) {  // no x . W product on this side: one instantiation
     k_trial_fast<1, 4, false, false><<<grid, kThreads, 0, s>>>(g, pass, zc, tgt, Q, x, Wsrc, found, part, nblk);
+    return;
+  }
+  if (trial_mx_ok(g)) {   // side 0 on the matrix cores
+    dim3 gr(nblk, 4, g.H / 128);
+    if (spec) k_trial_mx<true><<<gr, kThreads, 0, s>>>(g, pass, zc, tgt, x, Wsrc, found, part, nblk, sp);
+    else k_trial_mx<false><<<gr, kThreads, 0, s>>>(g, pass, zc, tgt, x, Wsrc, found, part, nblk, sp);
     return;
   }
   if (trial_rows_ok(g)) {

@@ -178,6 +178,9 @@ int stream_blocks(const Geom& g);   // grid (per gate) of the fast streaming pas
 // H % 256 == 0: the fast trial passes run as row-pair workgroups over H/256 column blocks, and
 // write stream_blocks(g) * H/256 partials per slot (the reduce's nblk)
 bool trial_rows_ok(const Geom& g);
+// H % 256 == 0, D <= 16: the x-side trial passes run on the matrix cores (k_trial_mx) over
+// H/128 column groups, writing stream_blocks(g) * H/128 partials per slot
+bool trial_mx_ok(const Geom& g);
 
 // after the x stage (fast path): zc += X dWx
 void launch_apply_dwx(const Geom& g, const float* x, const float* dW, float* zc, hipStream_t s);

@@ -283,18 +283,48 @@ __device__ unsigned long long g_sr_wait[2048][2];   // per workgroup: cycles the
 #define SR_SYNC() __syncthreads()
 #endif
 
-template <int NT, int XC>
+// ROWS = 32: tiles of 32 rows x 32 columns, v_mfma_f32_32x32x16_bf16 over 16-deep chunks
+//            (H <= 256: the two split A buffers of 32 rows fit the LDS).
+// ROWS = 16: tiles of 16 rows x 64 columns, v_mfma_f32_16x16x32_bf16 over 32-deep chunks
+//            (256 < H <= 512, the C5 shape; a gate's tile is four 16x16 products).
+template <int NT, int XC, int ROWS = 32>
 struct SrGeom {
-  static constexpr int H = 32 * NT, XK = 16 * XC, K2 = XK + H;
-  static constexpr int KC2 = K2 / 16;          // 16-deep chunks per tile
+  static constexpr int TW = ROWS == 32 ? 32 : 64;   // tile width (columns)
+  static constexpr int KD = ROWS == 32 ? 16 : 32;   // chunk depth
+  static constexpr int H = TW * NT, XK = KD * XC, K2 = XK + H;
+  static constexpr int KC2 = K2 / KD;          // chunks per tile
   static constexpr int AST = K2 + 8;           // A row stride (bf16): 16-B reads conflict-free over 16 rows
-  static constexpr int APIECE = SR_ROWS * AST; // one split piece of one A buffer
+  static constexpr int APIECE = ROWS * AST;    // one split piece of one A buffer
   static constexpr int GT = NT * KC2;          // chunks per t
-  static constexpr int U = GT % 8 == 0 ? 8 : GT % 4 == 0 ? 4 : GT % 3 == 0 ? 3 : GT % 2 == 0 ? 2 : 1;
+  static constexpr int U = ROWS == 16 ? (GT % 2 == 0 ? 2 : 1)   // 12 bf16x8 per chunk: a 2-deep ring
+                         : GT % 8 == 0 ? 8 : GT % 4 == 0 ? 4 : GT % 3 == 0 ? 3 : GT % 2 == 0 ? 2 : 1;
 };
 
 // B operand image: for gate q, tile n, chunk c, piece p and lane (h, c32) the 8 bf16
 // pieces of W[16c + 8h + j][32n + c32], j = 0..7, W = [Wx_q zero-padded to 16*XC rows; Wh_q].
+// ROWS = 16 image: for gate q, tile n, chunk c, column block jq, piece p and lane (kq, r16) the 8
+// bf16 pieces of W[32c + 8kq + j][64n + 16jq + r16] (the v_mfma_f32_16x16x32_bf16 B fragment).
+__global__ __launch_bounds__(kThreads) void k_sweep_wt16(int D, int H, int XC, Weights w, bf16x8* __restrict__ wt) {
+  const int NT = H / 64, KC2 = XC + H / 32, XK = 32 * XC;
+  const int total = 4 * NT * KC2 * 4 * 64;
+  for (int i = blockIdx.x * kThreads + threadIdx.x; i < total; i += gridDim.x * kThreads) {
+    const int lane = i & 63, jq = (i >> 6) & 3, c = (i >> 8) % KC2, n = (i / (256 * KC2)) % NT,
+              q = i / (256 * KC2 * NT);
+    const int jj = 64 * n + 16 * jq + (lane & 15), kb = 32 * c + 8 * (lane >> 4);
+    bf16x8 p0, p1, p2;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int k = kb + j;
+      const float v = k < XK ? (k < D ? w.wx[q][(int64_t)k * H + jj] : 0.f) : w.wh[q][(int64_t)(k - XK) * H + jj];
+      __bf16 a0, a1, a2;
+      split3(v, a0, a1, a2);
+      p0[j] = a0; p1[j] = a1; p2[j] = a2;
+    }
+    const int base = ((((q * NT + n) * KC2 + c) * 4 + jq) * 3) * 64 + lane;
+    wt[base] = p0; wt[base + 64] = p1; wt[base + 128] = p2;
+  }
+}
+
 __global__ __launch_bounds__(kThreads) void k_sweep_wt(int D, int H, int XC, Weights w, bf16x8* __restrict__ wt) {
   const int NT = H / 32, KC2 = XC + 2 * NT, XK = 16 * XC;
   const int total = 4 * NT * KC2 * 64;
@@ -321,15 +351,17 @@ __global__ __launch_bounds__(kThreads) void k_sweep_wt(int D, int H, int XC, Wei
 // leaves R of its tile in the z tile's LDS slot; two steps later the gate's producer wave folds
 // it in with 16 v_mfma_f32_16x16x4_f32 (K = the tile's 32 rows, M = d, N = 32 columns) into a
 // register ring of NT column tiles that turns once per tile.
-template <int NT, int XC, bool GX>
+template <int NT, int XC, bool GX, int ROWS = 32>
 __global__ __launch_bounds__(SR_THREADS) void k_sweep_rows(Geom g, const bf16x8* __restrict__ wt, Hyper hp,
                                                             SweepT a) {
-  using SG = SrGeom<NT, XC>;
+  using SG = SrGeom<NT, XC, ROWS>;
+  static_assert(ROWS == 32 || !GX, "the G_x fold is built for 32-row tiles");
   constexpr int H = SG::H, XK = SG::XK, K2 = SG::K2, KC2 = SG::KC2, AST = SG::AST, AP = SG::APIECE;
+  constexpr int TW = SG::TW, ZG = ROWS * TW;   // tile width; one gate's z tile (floats)
   __shared__ __attribute__((aligned(16))) __bf16 Ab[2][3 * AP];
-  __shared__ __attribute__((aligned(16))) float Zb[2][4 * SR_ROWS * 32];
+  __shared__ __attribute__((aligned(16))) float Zb[2][4 * ZG];
   const int T = g.T, D = g.D;
-  const int64_t m0 = a.r0 + (int64_t)blockIdx.x * SR_ROWS;
+  const int64_t m0 = a.r0 + (int64_t)blockIdx.x * ROWS;
   const int64_t rs = (int64_t)(T + 1) * H;
   const int64_t BTH = g.BT() * H;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -344,14 +376,70 @@ __global__ __launch_bounds__(SR_THREADS) void k_sweep_rows(Geom g, const bf16x8*
   };
 
   // A image for t = 1: [x_1 | h_0]
-  for (int i = threadIdx.x; i < SR_ROWS * K2; i += SR_THREADS) {
+  for (int i = threadIdx.x; i < ROWS * K2; i += SR_THREADS) {
     const int row = i / K2, k = i % K2;
     const int64_t b = min(m0 + row, a.r1 - 1);
     put_a(1, row, k, k < XK ? (k < D ? a.x[b * T * D + k] : 0.f) : a.S.p[5][b * rs + (k - XK)]);
   }
   __syncthreads();
 
-  if (wave < 4) {
+  if (ROWS == 16 && wave < 4) {
+    // ------------------------------------------------------------------ producer, 16-row tiles
+    // As below with the 16x16x32 shape: per 32-deep chunk one A fragment set (row lane % 16,
+    // k 8 (lane / 16) ..) and four column blocks of B, 4 x 6 MFMAs; a 2-deep ring of B chunks.
+    constexpr int GT = SG::GT, U = SG::U;
+    const int q = wave, r16 = lane & 15, kq = lane >> 4;
+    const bf16x8* wq = wt + (size_t)q * GT * 12 * 64 + lane;
+    bf16x8 bq[U][4][3];
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int p = 0; p < 3; ++p) bq[u][j][p] = wq[(u * 12 + j * 3 + p) * 64];
+    f32x4 acc[4] = {};
+    for (int t = 1; t <= T; ++t) {
+      const __bf16* A = &Ab[t & 1][r16 * AST + 8 * kq];
+#pragma unroll 1
+      for (int G0 = 0; G0 < GT; G0 += U) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const int G = G0 + u, n = G / KC2, cc = G - n * KC2;
+          if (n == 0 && cc == KC2 - 2) SR_SYNC();   // mid-step: h_{t-1} of tile NT-1 is in
+          const bf16x8 a0 = *reinterpret_cast<const bf16x8*>(A + 32 * cc);
+          const bf16x8 a1 = *reinterpret_cast<const bf16x8*>(A + AP + 32 * cc);
+          const bf16x8 a2 = *reinterpret_cast<const bf16x8*>(A + 2 * AP + 32 * cc);
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {   // smallest terms first
+            acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a2, bq[u][j][0], acc[j], 0, 0, 0);
+            acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, bq[u][j][1], acc[j], 0, 0, 0);
+            acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, bq[u][j][2], acc[j], 0, 0, 0);
+            acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, bq[u][j][0], acc[j], 0, 0, 0);
+            acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, bq[u][j][1], acc[j], 0, 0, 0);
+            acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, bq[u][j][0], acc[j], 0, 0, 0);
+          }
+          const int Gn = G + U < GT ? G + U : G + U - GT;
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int p = 0; p < 3; ++p) bq[u][j][p] = wq[(Gn * 12 + j * 3 + p) * 64];
+          if (cc == KC2 - 1) {   // C map: row 4 (lane / 16) + v, column 16 j + lane % 16
+            float* Z = &Zb[((t - 1) * NT + n) & 1][q * ZG + 4 * kq * TW + r16];
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+#pragma unroll
+              for (int v = 0; v < 4; ++v) Z[v * TW + 16 * j] = acc[j][v];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) acc[j] = f32x4{};
+            SR_SYNC();   // end of step
+          }
+        }
+      }
+    }
+    __syncthreads();         // final step: the consumer drains the last tile
+    return;
+  }
+  if (ROWS == 32 && wave < 4) {
     // ------------------------------------------------------------------ producer (gate q)
     // The B stream of a wave is the cyclic sequence of its GT chunks per t (3 x 16 B per lane
     // each).  The loop walks it U chunks at a time with a U-deep register ring: slot u holds
@@ -384,7 +472,7 @@ __global__ __launch_bounds__(SR_THREADS) void k_sweep_rows(Geom g, const bf16x8*
         const int tn = gxs / NT + 2;
         if (tn <= T) load_gx_x(tn, xnext);
       }
-      const float* Rq = &Zb[buf][q * SR_ROWS * 32 + (lane >> 4) * 32 + (lane & 15)];
+      const float* Rq = &Zb[buf][q * ZG + (lane >> 4) * 32 + (lane & 15)];
 #pragma unroll
       for (int ks = 0; ks < 8; ++ks)
 #pragma unroll
@@ -428,7 +516,7 @@ __global__ __launch_bounds__(SR_THREADS) void k_sweep_rows(Geom g, const bf16x8*
 #pragma unroll
           for (int p = 0; p < 3; ++p) bq[u][p] = wq[(Gn * 3 + p) * 64];
           if (cc == KC2 - 1) {
-            float* Z = &Zb[((t - 1) * NT + n) & 1][q * SR_ROWS * 32 + c];
+            float* Z = &Zb[((t - 1) * NT + n) & 1][q * ZG + c];
 #pragma unroll
             for (int r = 0; r < 16; ++r) Z[acc_row(r, lane) * 32] = acc[r];
             acc = f32x16{};
@@ -477,7 +565,8 @@ __global__ __launch_bounds__(SR_THREADS) void k_sweep_rows(Geom g, const bf16x8*
   // buffer descriptors: one 32-bit byte offset per thread serves every plane, and the record
   // count (rows < r1) turns loads past the last row into zeros and drops their stores.
   const int ct = threadIdx.x - 4 * 64;      // 0..255
-  const int row = ct >> 3, j4 = (ct & 7) * 4;
+  constexpr int TPR = TW / 4;               // threads per tile row (8 or 16)
+  const int row = ct / TPR, j4 = (ct % TPR) * 4;
   const uint32_t pbytes = (uint32_t)(a.r1 * rs * 4), zbytes = (uint32_t)(a.r1 * T * H * 4);
   __amdgpu_buffer_rsrc_t rS[6], rL[6];
 #pragma unroll
@@ -500,7 +589,7 @@ __global__ __launch_bounds__(SR_THREADS) void k_sweep_rows(Geom g, const bf16x8*
   const bool lh_zero = a.lamh_nz != nullptr && *a.lamh_nz == 0;
   struct St4 { f32x4 f0, g0, c0, h0, cp, li, lf, lg, lo, lc, lh; };
   auto load_tile = [&](int t, int n, St4& v) {
-    const uint32_t o = pofs + (uint32_t)(t * H + 32 * n) * 4;
+    const uint32_t o = pofs + (uint32_t)(t * H + TW * n) * 4;
     v.f0 = buf_ld4(rS[1], o); v.g0 = buf_ld4(rS[2], o); v.c0 = buf_ld4(rS[4], o); v.h0 = buf_ld4(rS[5], o);
     // c_{t-1}: from the state plane only at t = 1 (the initial c); later this thread's own
     // update of the previous t, kept in registers (cring)
@@ -509,11 +598,11 @@ __global__ __launch_bounds__(SR_THREADS) void k_sweep_rows(Geom g, const bf16x8*
     v.lo = buf_ld4(rL[3], o); v.lc = buf_ld4(rL[4], o);
     v.lh = lh_zero && t < T ? f32x4{} : buf_ld4(rL[5], o);
   };
-  // x_{tn} into A-buffer tn&1 (32 rows x XK)
+  // x_{tn} into A-buffer tn&1 (ROWS rows x XK)
   auto load_x = [&](int tn) {
     if (tn > T) return;
 #pragma unroll
-    for (int u = 0; u < 2 * XC; ++u) {
+    for (int u = 0; u < ROWS * XK / 256; ++u) {
       const int i = ct + 256 * u, xr = i / XK, k = i % XK;
       const int64_t b = min(m0 + xr, a.r1 - 1);
       put_a(tn & 1, xr, k, k < D ? a.x[(b * T + (tn - 1)) * D + k] : 0.f);
@@ -548,8 +637,9 @@ __global__ __launch_bounds__(SR_THREADS) void k_sweep_rows(Geom g, const bf16x8*
 #endif
       if (n + 1 < NT) load_tile(t, n + 1, nxt);
       else if (!last) load_tile(t + 1, 0, nxt);
-      f32x4* Z = reinterpret_cast<f32x4*>(&Zb[((t - 1) * NT + n) & 1][row * 32 + j4]);
-      const f32x4 zi = Z[0], zf = Z[SR_ROWS * 8], zg = Z[2 * SR_ROWS * 8], zo = Z[3 * SR_ROWS * 8];
+      f32x4* Z = reinterpret_cast<f32x4*>(&Zb[((t - 1) * NT + n) & 1][row * TW + j4]);
+      constexpr int ZG4 = ZG / 4;   // one gate's tile in f32x4
+      const f32x4 zi = Z[0], zf = Z[ZG4], zg = Z[2 * ZG4], zo = Z[3 * ZG4];
       f32x4 i1, f1, g1, o1, c1, h1, li, lf, lg, lo, lc;
       f32x4 ai, af, ag, ao, di, df, dg, dO;   // phi(z), phi'(z) (GX)
       const f32x4 cpv = t == 1 ? cur.cp : cring[0];
@@ -574,9 +664,9 @@ __global__ __launch_bounds__(SR_THREADS) void k_sweep_rows(Geom g, const bf16x8*
       if constexpr (GX) {   // R = (phi(z) - tgt) phi'(z) into the z slot (0 past the last row)
         const float m = rok ? 1.f : 0.f;
         Z[0] = (ai - ti) * di * m;
-        Z[SR_ROWS * 8] = (af - tf) * df * m;
-        Z[2 * SR_ROWS * 8] = (ag - tg) * dg * m;
-        Z[3 * SR_ROWS * 8] = (ao - to) * dO * m;
+        Z[ZG4] = (af - tf) * df * m;
+        Z[2 * ZG4] = (ag - tg) * dg * m;
+        Z[3 * ZG4] = (ao - to) * dO * m;
       }
 #ifdef SR_TIMING
       asm volatile("" :: "v"(i1), "v"(f1), "v"(g1), "v"(o1), "v"(c1), "v"(h1), "v"(li), "v"(lf), "v"(lg), "v"(lo), "v"(lc));
@@ -585,12 +675,12 @@ __global__ __launch_bounds__(SR_THREADS) void k_sweep_rows(Geom g, const bf16x8*
       if (!last) {
         bf16x4 p0, p1, p2;
         split3(h1, p0, p1, p2);
-        __bf16* d = An + 32 * n;
+        __bf16* d = An + TW * n;
         *reinterpret_cast<bf16x4*>(d) = p0;
         *reinterpret_cast<bf16x4*>(d + AP) = p1;
         *reinterpret_cast<bf16x4*>(d + 2 * AP) = p2;
       }
-      const uint32_t po = pofs + (uint32_t)(t * H + 32 * n) * 4, zo4 = zofs + (uint32_t)((t - 1) * H + 32 * n) * 4;
+      const uint32_t po = pofs + (uint32_t)(t * H + TW * n) * 4, zo4 = zofs + (uint32_t)((t - 1) * H + TW * n) * 4;
       buf_st4(rS[0], po, i1); buf_st4(rS[1], po, f1); buf_st4(rS[2], po, g1); buf_st4(rS[3], po, o1);
       buf_st4<0>(rS[4], po, c1);             // c_t: read by the next step's kernels
       if (!last) buf_st4<0>(rS[5], po, h1);
@@ -2292,27 +2382,57 @@ void launch_sweep_t(const Geom& g, int t, const Weights& w, const Hyper& hp, con
   else k_sweep_t<false><<<grid, kThreads, 0, s>>>(g, t, w, hp, a);
 }
 
+// 16-row tiles for 256 < H <= 512 (ADMM_SWEEP_R16=0: those shapes take the per-t sweep)
+static bool sweep_r16(const Geom& g) {
+  static int on = -1;
+  if (on < 0) {
+    const char* e = std::getenv("ADMM_SWEEP_R16");
+    on = e ? std::atoi(e) != 0 : 1;
+  }
+  return on && g.H > 256 && g.H <= 512 && g.H % 64 == 0;
+}
+
 bool sweep_rows_ok(const Geom& g) {
   // 32-bit buffer offsets: a [B][T+1][H] plane and a [B*T][H] z-cache plane in bytes
-  // H >= 64: a tile's c_{t-1} is read back from the state plane, stored NT = H/32 tiles earlier
-  return g.H % 32 == 0 && g.H >= 64 && g.H <= 256 && g.D <= 32 && g.B * (int64_t)g.TP() * g.H * 4 < (int64_t)UINT32_MAX &&
+  // NT >= 2 column tiles (the mid-step barrier protocol)
+  const bool shape = (g.H % 32 == 0 && g.H >= 64 && g.H <= 256) || sweep_r16(g);
+  return shape && g.D <= 32 && g.B * (int64_t)g.TP() * g.H * 4 < (int64_t)UINT32_MAX &&
          4 * g.BT() * g.H * 4 < (int64_t)UINT32_MAX;   // the 4-plane z cache / target descriptors
 }
 
-static int sweep_xc(const Geom& g) { return (g.D + 15) / 16; }
+bool sweep_rows_gx_ok(const Geom& g) { return sweep_rows_ok(g) && !sweep_r16(g) && g.D <= 16; }
+
+static int sweep_xc(const Geom& g) { return sweep_r16(g) ? (g.D + 31) / 32 : (g.D + 15) / 16; }
 
 size_t sweep_wt_floats(const Geom& g) {   // bf16x8 image, in float units
+  if (sweep_r16(g)) return (size_t)4 * (g.H / 64) * (sweep_xc(g) + g.H / 32) * 4 * 3 * 64 * 4;
   return (size_t)4 * (g.H / 32) * (sweep_xc(g) + 2 * (g.H / 32)) * 3 * 64 * 4;
 }
 
 void launch_sweep_wt(const Geom& g, const Weights& w, float* wt, hipStream_t s) {
-  const int xc = sweep_xc(g), NT = g.H / 32;
+  const int xc = sweep_xc(g);
+  if (sweep_r16(g)) {
+    const int total = 4 * (g.H / 64) * (xc + g.H / 32) * 4 * 64;
+    k_sweep_wt16<<<cdiv64(total, kThreads), kThreads, 0, s>>>(g.D, g.H, xc, w, reinterpret_cast<bf16x8*>(wt));
+    return;
+  }
+  const int NT = g.H / 32;
   const int total = 4 * NT * (xc + 2 * NT) * 64;
   k_sweep_wt<<<cdiv64(total, kThreads), kThreads, 0, s>>>(g.D, g.H, xc, w, reinterpret_cast<bf16x8*>(wt));
 }
 
 template <int XC>
 static void launch_sweep_rows_xc(const Geom& g, const bf16x8* wt, const Hyper& hp, const SweepT& a, hipStream_t s) {
+  if (sweep_r16(g)) {
+    dim3 grid(cdiv64(a.r1 - a.r0, 16));
+    switch (g.H / 64) {
+#define SR16_CASE(N) case N: k_sweep_rows<N, XC, false, 16><<<grid, SR_THREADS, 0, s>>>(g, wt, hp, a); break;
+      SR16_CASE(5) SR16_CASE(6) SR16_CASE(7) SR16_CASE(8)
+#undef SR16_CASE
+      default: break;
+    }
+    return;
+  }
   dim3 grid(cdiv64(a.r1 - a.r0, SR_ROWS));
   switch (g.H / 32) {
 #define SR_CASE(N) case N: \

@@ -64,9 +64,15 @@ def make_data(gen: str, B: int, T: int, D: int, seed_offset: int = 0):
     return s[idx].unsqueeze(2).contiguous(), s[torch.arange(B) + T].unsqueeze(1).contiguous()
 
 
+def persistent_sweep(H: int) -> bool:
+    """k_sweep_rows: 32-row tiles for 64 <= H <= 256, 16-row tiles for 256 < H <= 512 (H % 64 == 0)."""
+    r16 = 256 < H <= 512 and H % 64 == 0 and os.environ.get('ADMM_SWEEP_R16', '1') != '0'
+    return os.environ.get('ADMM_SWEEP_ROWS', '1') != '0' and ((64 <= H <= 256 and H % 32 == 0) or r16)
+
+
 def tgt_from_sweep(H: int) -> bool:
-    """The persistent sweep (64 <= H <= 256) writes the next x stage's targets unless disabled."""
-    return 64 <= H <= 256 and os.environ.get('ADMM_TGT_SWEEP', '1') != '0'
+    """The persistent sweep writes the next x stage's targets unless disabled."""
+    return persistent_sweep(H) and os.environ.get('ADMM_TGT_SWEEP', '1') != '0'
 
 
 def roofline_terms(cls: str, B: int, T: int, D: int, H: int):
@@ -84,7 +90,7 @@ def roofline_terms(cls: str, B: int, T: int, D: int, H: int):
         # X^T R partials: x once more, and a [blocks][4][D][H] slab.
         lamh_all = os.environ.get('ADMM_LAMH_SKIP', '1') == '0'
         byts = T * f4 * B * (D + (29 if lamh_all else 28) * H) + f4 * B * (1 if lamh_all else 2) * H
-        if D <= 16 and os.environ.get('ADMM_GX_SWEEP', '1') != '0':
+        if D <= 16 and H <= 256 and os.environ.get('ADMM_GX_SWEEP', '1') != '0':
             byts += f4 * B * T * D + f4 * ((B + 31) // 32) * 4 * D * H
         return flops, byts
     n = float(B) * T * H          # elements of one [B*T, H] plane

@@ -515,6 +515,44 @@ def test_persistent_sweep_matches_per_t_sweep(lamh_edit, mods, dev, monkeypatch)
             assert d <= 1e-5 * scale, (k, q, d, scale)
 
 
+@pytest.mark.parametrize('shape', [(200, 5, 1, 512), (77, 3, 16, 384), (64, 4, 5, 320)])
+def test_persistent_sweep_r16_matches_per_t_sweep(shape, mods, dev, monkeypatch):
+    """256 < H <= 512 (the C5 shape): the persistent sweep on 16-row x 64-column tiles
+    (v_mfma_f32_16x16x32_bf16, split3) against the per-t sweep (ADMM_SWEEP_R16=0, f32 MFMA) over
+    three steps of the no_dual_y variant on random-walk windows: same exponents, state within
+    fp32 rounding.  B % 16 != 0 covers the ragged last row block, D = 16 the x chunk padding."""
+    from blocks.lstm import LSTM
+    from parameters import example_parameter_dictionary
+    _, nd = mods
+    B, T, D, H = shape
+    g = torch.Generator().manual_seed(7)
+    s_ = torch.cumsum(torch.randn(B + T + 1, generator=g), 0)
+    s_ = (s_ - s_.min()) / (s_.max() - s_.min())
+    idx = torch.arange(B).unsqueeze(1) + torch.arange(T).unsqueeze(0)
+    x = s_[idx].unsqueeze(2).expand(B, T, D).contiguous().to(dev)
+    y = s_[torch.arange(B) + T].unsqueeze(1).contiguous().to(dev)
+    pd = example_parameter_dictionary['GoogleStock']
+    out = {}
+    for flag in ('1', '0'):
+        monkeypatch.setenv('ADMM_SWEEP_R16', flag)
+        torch.manual_seed(0)
+        m = LSTM(D, H, 1).to(dev)
+        opt = nd.ADMMBasedOptimizer(m, (x, y), pd, verbose=False)
+        ks = []
+        for _ in range(3):
+            opt.step()
+            ks.append(list(opt.last_step_stats()['k'].values()))
+        out[flag] = (ks, {q: opt.gates[q].clone() for q in GATES6}, {q: opt.duals[q].clone() for q in GATES6})
+        del opt
+    assert out['1'][0] == out['0'][0]
+    for k in (1, 2):
+        for q in GATES6:
+            a, b = out['1'][k][q], out['0'][k][q]
+            assert torch.isfinite(a).all(), q
+            d = float((a - b).abs().max())
+            assert d <= 1e-5 * max(1.0, float(b.abs().max())), (k, q, d)
+
+
 @pytest.mark.parametrize('lamh_edit', [False, True])
 def test_lamh_skip_bit_identical(lamh_edit, mods, dev, monkeypatch):
     """The persistent sweep's skip of the h dual's loads before T (zero there unless written from

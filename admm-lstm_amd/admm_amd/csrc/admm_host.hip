@@ -118,6 +118,10 @@ struct AdmmCtx {
   bool sweep_rows = false; // whole sweep as one persistent launch (k_sweep_rows; ADMM_SWEEP_ROWS=0 disables)
   float* swt = nullptr;    // its B-operand image of the weights
   bool split3 = false;     // h-stage GEMMs on split bf16 MFMAs (admm_split3.hip; ADMM_SPLIT3=0 disables)
+  // split pieces of the trial direction GEMM Q = Hprev G (ADMM_Q_PIECES=3: f32-accurate).  Q only
+  // enters the line-search increments, where 2^-16 relative is far inside the reference's own
+  // rounding of W + G/theta (DESIGN.md "trial direction precision"); G itself stays split3.
+  int q_pieces = 2;
   float* gimg = nullptr;   // split image of G_h for k_qgemm3
   hipStream_t sx[kMaxSweepStreams - 1] = {};
   hipEvent_t ev_fork = nullptr, ev_join[kMaxSweepStreams - 1] = {};
@@ -295,7 +299,7 @@ int stage_weights(AdmmCtx* c, int side, hipStream_t s) {
   // 2. trial direction Q = A G (not needed on the fast x side: formed inside the trials)
   if (!(fast && side == 0)) {
     ProfScope ps(c, side == 0 ? ADMM_PROF_QGEMM_X : ADMM_PROF_QGEMM_H, s);
-    if (side == 1 && c->split3) launch_qgemm3(g, c->buf.gates[ADMM_H], c->G, c->gimg, c->Q, s);
+    if (side == 1 && c->split3) launch_qgemm3(g, c->buf.gates[ADMM_H], c->G, c->gimg, c->Q, s, c->q_pieces);
     else launch_qgemm(g, side, c->buf.x, c->buf.gates[ADMM_H], c->G, c->Q, s);
   }
   // 3. line search: trial passes of kTrialJ exponents each until every gate has passed
@@ -456,6 +460,7 @@ int admm_create(const AdmmDims* dims, const AdmmParams* params, int device, Admm
   c->spec_x = fast_path(g) && trial_rows_ok(g);
   if (const char* e = std::getenv("ADMM_SPEC_X")) c->spec_x = c->spec_x && std::atoi(e) != 0;
   if (const char* e = std::getenv("ADMM_SPLIT3")) c->split3 = c->split3 && std::atoi(e) != 0;
+  if (const char* e = std::getenv("ADMM_Q_PIECES")) c->q_pieces = std::atoi(e) == 2 ? 2 : 3;
   Hyper& h = c->hp;
   for (int i = 0; i < 7; ++i) h.rho[i] = params->rho[i];
   for (int q = 0; q < 4; ++q) {

@@ -196,10 +196,14 @@ size_t split3_gimg_floats(const Geom& g);
 int atr3_splits(const Geom& g);
 void launch_atr3(const Geom& g, const float* Sh, const float* zc, const float* tgt, float* slab, int nsplit,
                  hipStream_t s);
-void launch_qgemm3(const Geom& g, const float* Sh, const float* G, float* gimg, float* Q, hipStream_t s);
+// pieces = 3: f32-accurate split3 products; 2: two-way splits, three products (~2^-16 relative),
+// enough for the trial direction ("trial direction precision")
+void launch_qgemm3(const Geom& g, const float* Sh, const float* G, float* gimg, float* Q, hipStream_t s,
+                   int pieces = 3);
 // the two halves of launch_qgemm3: G -> split image, then Q = Hprev G (gates with found[q] set skipped)
 void launch_split_g(const Geom& g, const float* G, float* gimg, hipStream_t s);
-void launch_qgemm3_img(const Geom& g, const float* Sh, const float* gimg, float* Q, const int* found, hipStream_t s);
+void launch_qgemm3_img(const Geom& g, const float* Sh, const float* gimg, float* Q, const int* found, hipStream_t s,
+                       int pieces = 3);
 // decide the first passing k in this pass's window; on success update the weights
 struct SelectArgs {
   int side;                 // 0 x, 1 h

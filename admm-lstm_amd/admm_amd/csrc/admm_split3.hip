@@ -49,6 +49,7 @@ __global__ __launch_bounds__(kThreads) void k_split_g(int H, const float* __rest
 // One 128 x 256 tile of one gate per workgroup (qgemm3_tile).  found != nullptr: gates whose
 // line search has already decided are skipped (the later trial passes, when pass 0 ran fused
 // in k_qtrial3 and Q was never formed).
+template <int NP>
 __global__ __launch_bounds__(kThreads) void k_qgemm3(Geom g, const float* __restrict__ Sh,
                                                       const bf16x8* __restrict__ gi, float* __restrict__ Q,
                                                       const int* __restrict__ found) {
@@ -61,7 +62,7 @@ __global__ __launch_bounds__(kThreads) void k_qgemm3(Geom g, const float* __rest
   if (found && found[q]) return;
   const int64_t m0 = (int64_t)(lid / 4) * Q3_BM, BT = g.BT();
   f32x16 acc[2][4];
-  qgemm3_tile(g, Sh, gi, q, cb, m0, lds, acc);
+  qgemm3_tile<NP>(g, Sh, gi, q, cb, m0, lds, acc);
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, wr = wave >> 1, wc = wave & 1, c32 = lane & 31;
   float* Qq = Q + (int64_t)q * BT * H + Q3_BN * cb + wc * 128 + c32;
 #pragma unroll
@@ -320,15 +321,17 @@ void launch_split_g(const Geom& g, const float* G, float* gimg, hipStream_t s) {
   k_split_g<<<(total + kThreads - 1) / kThreads, kThreads, 0, s>>>(g.H, G, reinterpret_cast<bf16x8*>(gimg));
 }
 
-void launch_qgemm3_img(const Geom& g, const float* Sh, const float* gimg, float* Q, const int* found, hipStream_t s) {
+void launch_qgemm3_img(const Geom& g, const float* Sh, const float* gimg, float* Q, const int* found, hipStream_t s,
+                       int pieces) {
   const int64_t nrt = (g.BT() + Q3_BM - 1) / Q3_BM;
   dim3 grid((unsigned)(nrt * 4 * (g.H / Q3_BN)));
-  k_qgemm3<<<grid, kThreads, 0, s>>>(g, Sh, reinterpret_cast<const bf16x8*>(gimg), Q, found);
+  if (pieces == 2) k_qgemm3<2><<<grid, kThreads, 0, s>>>(g, Sh, reinterpret_cast<const bf16x8*>(gimg), Q, found);
+  else k_qgemm3<3><<<grid, kThreads, 0, s>>>(g, Sh, reinterpret_cast<const bf16x8*>(gimg), Q, found);
 }
 
-void launch_qgemm3(const Geom& g, const float* Sh, const float* G, float* gimg, float* Q, hipStream_t s) {
+void launch_qgemm3(const Geom& g, const float* Sh, const float* G, float* gimg, float* Q, hipStream_t s, int pieces) {
   launch_split_g(g, G, gimg, s);
-  launch_qgemm3_img(g, Sh, gimg, Q, nullptr, s);
+  launch_qgemm3_img(g, Sh, gimg, Q, nullptr, s, pieces);
 }
 
 }  // namespace admm

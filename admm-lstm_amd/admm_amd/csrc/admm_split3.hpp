@@ -29,17 +29,27 @@ __device__ __forceinline__ f32x16 mfma_split3(const bf16x8 (&a)[3], const bf16x8
   return acc;
 }
 
+// the three products of two-way splits (a = a0 + a1, b = b0 + b1 to ~2^-17): a0 b0 + a0 b1 + a1 b0,
+// ~2^-16 relative -- for the trial direction Q only (see k_qgemm3)
+__device__ __forceinline__ f32x16 mfma_split2(const bf16x8 (&a)[3], const bf16x8 (&b)[3], f32x16 acc) {
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], b[0], acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[1], acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[0], acc, 0, 0, 0);
+  return acc;
+}
+
 __device__ __forceinline__ void frag3(const __bf16* img, int piece_stride, int off, bf16x8 (&f)[3]) {
 #pragma unroll
   for (int p = 0; p < 3; ++p) f[p] = *reinterpret_cast<const bf16x8*>(img + p * piece_stride + off);
 }
 
+template <int NP = 3>
 __device__ __forceinline__ void put3(__bf16* img, int piece_stride, int off, f32x8 v) {
   bf16x8 p0, p1, p2;
   split3(v, p0, p1, p2);
   *reinterpret_cast<bf16x8*>(img + off) = p0;
   *reinterpret_cast<bf16x8*>(img + piece_stride + off) = p1;
-  *reinterpret_cast<bf16x8*>(img + 2 * piece_stride + off) = p2;
+  if (NP == 3) *reinterpret_cast<bf16x8*>(img + 2 * piece_stride + off) = p2;
 }
 
 // ------------------------------------------------------------------ Q tile = Hprev G
@@ -54,6 +64,8 @@ constexpr int kQ3AP = Q3_BM * 16;               // one piece of the A image (bf1
 constexpr int kQ3BU = (Q3_BN / 32) * 3 * 64;    // bf16x8 units of one B step image
 constexpr int kQ3Lds = 2 * 3 * kQ3AP * 2 + 2 * kQ3BU * 16;
 
+// NP = 3: the six split3 products (f32-accurate); NP = 2: mfma_split2 (half the matrix work).
+template <int NP>
 __device__ __forceinline__ void qgemm3_tile(const Geom& g, const float* __restrict__ Sh,
                                             const bf16x8* __restrict__ gi, int q, int cb, int64_t m0,
                                             char* lds, f32x16 (&acc)[2][4]) {
@@ -82,7 +94,7 @@ __device__ __forceinline__ void qgemm3_tile(const Geom& g, const float* __restri
     for (int u = 0; u < BU / kThreads; ++u) rb[u] = bp[c * bstep + u * kThreads];
   };
   auto lstore = [&](int st) {
-    put3(As + st * 3 * AP, AP, sw_off(sr, sh), f32x8{ra0.x, ra0.y, ra0.z, ra0.w, ra1.x, ra1.y, ra1.z, ra1.w});
+    put3<NP>(As + st * 3 * AP, AP, sw_off(sr, sh), f32x8{ra0.x, ra0.y, ra0.z, ra0.w, ra1.x, ra1.y, ra1.z, ra1.w});
 #pragma unroll
     for (int u = 0; u < BU / kThreads; ++u) Bs[st * BU + tid + u * kThreads] = rb[u];
   };
@@ -98,13 +110,20 @@ __device__ __forceinline__ void qgemm3_tile(const Geom& g, const float* __restri
 #pragma unroll
     for (int mi = 0; mi < 2; ++mi) {
       bf16x8 a[3];
-      frag3(As + st * 3 * AP, AP, sw_off(wr * 64 + mi * 32 + c32, kh), a);
+      if (NP == 3) {
+        frag3(As + st * 3 * AP, AP, sw_off(wr * 64 + mi * 32 + c32, kh), a);
+      } else {
+        const int o = sw_off(wr * 64 + mi * 32 + c32, kh);
+        a[0] = *reinterpret_cast<const bf16x8*>(As + st * 3 * AP + o);
+        a[1] = *reinterpret_cast<const bf16x8*>(As + st * 3 * AP + AP + o);
+      }
 #pragma unroll
       for (int ni = 0; ni < 4; ++ni) {
         const bf16x8* bb = &Bs[st * BU + (wc * 4 + ni) * 192 + lane];
-        const bf16x8 b[3] = {bb[0], bb[64], bb[128]};
+        const bf16x8 b[3] = {bb[0], bb[64], NP == 3 ? bb[128] : bb[0]};
         if (S3_ABL & 64) acc[mi][ni][0] += (float)a[0][0] * (float)b[0][0];
-        else acc[mi][ni] = mfma_split3(a, b, acc[mi][ni]);
+        else if (NP == 3) acc[mi][ni] = mfma_split3(a, b, acc[mi][ni]);
+        else acc[mi][ni] = mfma_split2(a, b, acc[mi][ni]);
       }
     }
     __builtin_amdgcn_sched_barrier(0);

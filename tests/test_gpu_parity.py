@@ -786,6 +786,37 @@ def test_sweep_gx_matches_resid_pass(shape, D_, mods, dev, monkeypatch):
     assert out[1][3] == pytest.approx(out[0][3], rel=1e-5)
 
 
+@pytest.mark.parametrize('shape', [(500, 3, 16, 256), (256, 4, 1, 512)])
+def test_q_two_piece_split_same_trajectory(shape, mods, dev, monkeypatch):
+    """The h-side trial direction Q = Hprev G_h on two-way bf16 splits (three products, ~2^-16
+    relative; the default) against the f32-accurate split3 GEMM (ADMM_Q_PIECES=3).  Q enters only
+    the line-search increments, so with the same exponents the trajectories are bitwise equal:
+    over several steps every exponent must agree, and then weights and state are identical."""
+    from blocks.lstm import LSTM
+    from parameters import example_parameter_dictionary
+    admm, _ = mods
+    admm.with_dual_y = False
+    B, T, D, H = shape
+    g = torch.Generator().manual_seed(19)
+    x = torch.rand(B, T, D, generator=g).to(dev)
+    y = (0.8 * x.mean((1, 2)).unsqueeze(1) + 0.1 * torch.rand(B, 1, generator=g).to(dev)).contiguous()
+    out = []
+    for mode in ('3', '2'):
+        monkeypatch.setenv('ADMM_Q_PIECES', mode)
+        torch.manual_seed(0)
+        m = LSTM(D, H, 1).to(dev)
+        opt = admm.ADMMBasedOptimizer(m, (x, y), example_parameter_dictionary['GoogleStock'], verbose=False)
+        ks = []
+        for _ in range(5):
+            opt.step()
+            ks.append(list(opt.last_step_stats()['k'].values()))
+        out.append((ks, torch.cat([p.detach().flatten() for p in m.parameters()]
+                                  + [v.flatten() for v in opt.gates.values()])))
+        del opt
+    assert out[0][0] == out[1][0]
+    assert torch.equal(out[0][1], out[1][1])
+
+
 def test_generic_weight_stage_matches_fast(mods, dev, monkeypatch):
     """ADMM_GENERIC=1 runs the weight stages on the generic kernels (materialised R and Q, f32 MFMA
     GEMMs) instead of the fast streaming path.  Step 1 decides identically on both: the x-side

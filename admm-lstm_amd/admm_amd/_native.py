@@ -27,7 +27,7 @@ NCCL_UNIQUE_ID_BYTES = 128
 
 # kernel classes of admm_profile (include/admm_lstm.h)
 PROF_CLASSES = ('sweep', 'trial', 'trial_extra', 'atr_x', 'atr_h', 'qgemm_x', 'qgemm_h', 'resid', 'small',
-                'zgemm', 'comm')
+                'zgemm', 'comm', 'trial_h')
 
 
 class NativeUnavailable(RuntimeError):

@@ -320,7 +320,7 @@ int stage_weights(AdmmCtx* c, int side, hipStream_t s) {
                    : fast && trial_rows_ok(g) ? nblk * (g.H / 256) : nblk;
   for (int pass = 0; pass < kMaxPasses; ++pass) {
     {
-      ProfScope ps(c, pass == 0 ? ADMM_PROF_TRIAL : ADMM_PROF_TRIAL_EXTRA, s);
+      ProfScope ps(c, pass > 0 ? ADMM_PROF_TRIAL_EXTRA : side == 0 ? ADMM_PROF_TRIAL : ADMM_PROF_TRIAL_H, s);
       SpecX sx{};
       if (spec && side == 0 && pass == 0) {
         sx.kpred = c->kpred;

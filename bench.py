@@ -102,18 +102,20 @@ def roofline_terms(cls: str, B: int, T: int, D: int, H: int):
         return 2.0 * B * T * H * 4 * H, f4 * (B * T * H + 4 * n)
     if cls == 'qgemm_x':
         return 2.0 * B * T * D * 4 * H, f4 * (B * T * D + 4 * n)
-    if cls in ('trial', 'trial_extra'):  # read z, tgt, Q per element
+    if cls in ('trial', 'trial_h', 'trial_extra'):
+        # three planes per gate either way: pass 0 of the x side reads z and tgt and (H % 256 == 0)
+        # writes the h stage's residual R_h for the predicted exponent; the h side reads z, tgt and Q
         return 0.0, f4 * 3 * 4 * n
     if cls == 'resid':            # x-stage residual (read z and tgt, or z, lam, S and write tgt) + z += X dWx
         return 0.0, f4 * ((2 if tgt else 4) + 2) * 4 * n
-    # trials: pass 0 of the x side reads z and tgt and (H % 256 == 0) writes z + x dWx for the
-    # predicted exponent; the h side reads z, tgt and Q -- three planes per gate either way
     return None
 
 
 # kernel symbols of each profile class (admm_kernels.hip), for the committed PMC traffic
 CLASS_KERNELS = {'sweep': ('k_sweep_rows', 'k_sweep_t'), 'atr_h': ('k_atr3', 'k_atr_fused', 'k_atr<128'), 'qgemm_h': ('k_qgemm3', 'k_qgemm<true, 1>'),
-                 'trial': ('k_trial_rows', 'k_trial_fast', 'k_trial<'), 'resid': ('k_resid_gx', 'k_apply_dwx', 'k_resid<')}
+                 'trial': ('k_trial_mx<true>', 'k_trial_rows<0', 'k_trial_fast<0', 'k_trial<'),
+                 'trial_h': ('k_trial_rows<1', 'k_trial_fast<1', 'k_trial<'),
+                 'resid': ('k_resid_gx', 'k_apply_dwx', 'k_resid<')}
 
 
 def pmc_traffic(cls: str, cfg_name: str):
@@ -127,7 +129,7 @@ def pmc_traffic(cls: str, cfg_name: str):
         return None
     kern = json.load(open(files[-1]))['kernels']
     # trial passes after the first return early (gates already decided): use the full pass
-    key = 'traffic_bytes_max' if cls == 'trial' else 'traffic_bytes_median'
+    key = 'traffic_bytes_max' if cls in ('trial', 'trial_h') else 'traffic_bytes_median'
     for prefix in CLASS_KERNELS[cls]:     # the first kernel family present in the profile
         vals = [v[key] for k, v in kern.items() if k.startswith(prefix)]
         if vals:
@@ -179,7 +181,7 @@ def main():
     ap.add_argument('--config', default='c3', choices=sorted(CONFIGS))
     ap.add_argument('--scaling', default='weak', choices=['weak', 'strong'])
     ap.add_argument('--no-cpu-baseline', action='store_true')
-    ap.add_argument('--profile-classes', default='sweep,trial,trial_extra,atr_x,atr_h,qgemm_x,qgemm_h,resid,small')
+    ap.add_argument('--profile-classes', default='sweep,trial,trial_h,trial_extra,atr_x,atr_h,qgemm_x,qgemm_h,resid,small')
     args = ap.parse_args()
 
     world = int(os.environ.get('WORLD_SIZE', '1'))

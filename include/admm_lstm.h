@@ -156,7 +156,7 @@ int admm_poll_status(AdmmCtx* ctx, int32_t* unresolved, int32_t* nonfinite);
    resets.  Classes: */
 enum {
   ADMM_PROF_SWEEP = 0,        /* k_sweep_t, one launch per time step t */
-  ADMM_PROF_TRIAL = 1,        /* first line-search trial pass (x and h stages) */
+  ADMM_PROF_TRIAL = 1,        /* first line-search trial pass of the x stage */
   ADMM_PROF_TRIAL_EXTRA = 2,  /* later trial passes (no-ops once every gate is resolved) */
   ADMM_PROF_ATR_X = 3,        /* G = X^T R (x stage) */
   ADMM_PROF_ATR_H = 4,        /* G = Hprev^T R (h stage) */
@@ -166,7 +166,8 @@ enum {
   ADMM_PROF_SMALL = 8,        /* wy and h_T kernels */
   ADMM_PROF_ZGEMM = 9,        /* z-cache recompute (only after external modifications) */
   ADMM_PROF_COMM = 10,        /* RCCL all-reduces */
-  ADMM_PROF_CLASSES = 11
+  ADMM_PROF_TRIAL_H = 11,     /* first line-search trial pass of the h stage */
+  ADMM_PROF_CLASSES = 12
 };
 int admm_profile(AdmmCtx* ctx, uint32_t class_mask);
 int admm_profile_read(AdmmCtx* ctx, double* ms /* [ADMM_PROF_CLASSES] */, int32_t* count /* [ADMM_PROF_CLASSES] */);

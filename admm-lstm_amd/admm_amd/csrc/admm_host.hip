@@ -122,6 +122,7 @@ struct AdmmCtx {
   // enters the line-search increments, where 2^-16 relative is far inside the reference's own
   // rounding of W + G/theta (DESIGN.md "trial direction precision"); G itself stays split3.
   int q_pieces = 2;
+  bool atr3w = true;       // k_atr3w (two waves per SIMD) for the h-side gradient; ADMM_ATR3W=0: k_atr3
   float* gimg = nullptr;   // split image of G_h for k_qgemm3
   hipStream_t sx[kMaxSweepStreams - 1] = {};
   hipEvent_t ev_fork = nullptr, ev_join[kMaxSweepStreams - 1] = {};
@@ -269,7 +270,7 @@ int stage_weights(AdmmCtx* c, int side, hipStream_t s) {
   } else if (fast && c->split3) {
     ns = atr3_splits(g);
     ProfScope ps(c, ADMM_PROF_ATR_H, s);
-    launch_atr3(g, c->buf.gates[ADMM_H], zh, c->tgt, c->gslab, ns, s);
+    launch_atr3(g, c->buf.gates[ADMM_H], zh, c->tgt, c->gslab, ns, s, c->atr3w);
   } else if (fast) {
     ns = atr_splits(g, 1);
     ProfScope ps(c, ADMM_PROF_ATR_H, s);
@@ -460,6 +461,7 @@ int admm_create(const AdmmDims* dims, const AdmmParams* params, int device, Admm
   c->spec_x = fast_path(g) && trial_rows_ok(g);
   if (const char* e = std::getenv("ADMM_SPEC_X")) c->spec_x = c->spec_x && std::atoi(e) != 0;
   if (const char* e = std::getenv("ADMM_SPLIT3")) c->split3 = c->split3 && std::atoi(e) != 0;
+  if (const char* e = std::getenv("ADMM_ATR3W")) c->atr3w = std::atoi(e) != 0;
   if (const char* e = std::getenv("ADMM_Q_PIECES")) c->q_pieces = std::atoi(e) == 2 ? 2 : 3;
   Hyper& h = c->hp;
   for (int i = 0; i < 7; ++i) h.rho[i] = params->rho[i];

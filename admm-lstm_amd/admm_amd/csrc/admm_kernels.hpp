@@ -194,8 +194,11 @@ void launch_atr_fused(const Geom& g, const Hyper& hp, const float* x, const floa
 bool split3_ok(const Geom& g);
 size_t split3_gimg_floats(const Geom& g);
 int atr3_splits(const Geom& g);
+// two_waves (H == 256, atr3w_ok): k_atr3w, 8 waves with 128 accumulators (two per SIMD) instead of
+// k_atr3's 4 with 256; the same products in the same order, so bit-identical slabs
+bool atr3w_ok(const Geom& g);
 void launch_atr3(const Geom& g, const float* Sh, const float* zc, const float* tgt, float* slab, int nsplit,
-                 hipStream_t s);
+                 hipStream_t s, bool two_waves = true);
 // pieces = 3: f32-accurate split3 products; 2: two-way splits, three products (~2^-16 relative),
 // enough for the trial direction ("trial direction precision")
 void launch_qgemm3(const Geom& g, const float* Sh, const float* G, float* gimg, float* Q, hipStream_t s,

@@ -294,6 +294,142 @@ __global__ __launch_bounds__(kThreads, A3<A3_BN>::MINB) void k_atr3(Geom g, cons
     atr3_body<false, A3_BN>(g, mb, nb, q, sp, nsplit, Sh, zc + q * n, tgt + q * n, slab, img);
 }
 
+// ------------------------------------------------------------------ slab = Hprev^T R, two waves per SIMD
+// The same tile, images and fragment reads as k_atr3 (256 m x 256 j of one gate, 16-row steps),
+// but 8 waves as 2 (m) x 4 (j) of 128 x 64: 128 accumulators per lane, so two waves share each
+// SIMD and one wave's staging VALU (phi, phi', the split3 of R and Hprev) and waits issue while
+// the other's MFMAs run.  At one wave per SIMD (k_atr3) the staging and the MFMAs of a wave
+// serialise.  Each wave stages two rows of each operand per step (one 1-KB row per
+// wave-instruction), two steps ahead through a two-slot register ring.
+constexpr int A3W_THREADS = 512;
+struct Atr3wRing { float4 a[2], z[2], t[2]; };
+
+template <bool TANH>
+__device__ __forceinline__ void atr3w_body(const Geom& g, int q, int sp, int nsplit, const float* __restrict__ Sh,
+                                           const float* __restrict__ zq, const float* __restrict__ tq,
+                                           float* __restrict__ slab, __bf16* img) {
+  using P = A3<256>;
+  const int H = g.H;
+  const int64_t BT = g.BT();
+  const int64_t per = ((BT + nsplit - 1) / nsplit + A3_KS - 1) / A3_KS * A3_KS;
+  const int64_t r0 = sp * per, r1 = r0 + per < BT ? r0 + per : BT;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int rg = __builtin_amdgcn_readfirstlane(wave);   // rows 2 rg, 2 rg + 1 of each step
+  const __amdgpu_buffer_rsrc_t rA = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(Sh), 0,
+                                                                      (int)(g.B * g.TP() * H * 4), kBufWord3);
+  const __amdgpu_buffer_rsrc_t rZ = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(zq), 0, (int)(BT * H * 4), kBufWord3);
+  const __amdgpu_buffer_rsrc_t rT = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(tq), 0, (int)(BT * H * 4), kBufWord3);
+  const int vo = 16 * lane;   // float4 column 4 lane of a 256-float row
+  auto gload = [&](Atr3wRing& R, int64_t k0) {   // rows past r1 clamped; they meet R = 0 in put()
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int64_t r = k0 + 2 * rg + i, row = r < r1 ? r : r1 - 1;
+      R.a[i] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rA, vo, (int)(g.hrow(row) * H * 4), 0));
+      R.z[i] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rZ, vo, (int)(row * H * 4), 2));
+      R.t[i] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rT, vo, (int)(row * H * 4), 2));
+    }
+  };
+  auto put = [&](int st, const Atr3wRing& R, int64_t k0) {
+    __bf16* A = img + st * P::STAGE;
+    __bf16* B = A + 3 * P::PA;
+    bf16x4 p0, p1, p2;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int rr = 2 * rg + i;
+      const int o = a3_off(rr, 4 * lane);
+      split3(f32x4{R.a[i].x, R.a[i].y, R.a[i].z, R.a[i].w}, p0, p1, p2);
+      *reinterpret_cast<bf16x4*>(A + o) = p0;
+      *reinterpret_cast<bf16x4*>(A + P::PA + o) = p1;
+      *reinterpret_cast<bf16x4*>(A + 2 * P::PA + o) = p2;
+      const bool ok = k0 + rr < r1;
+      const float zz[4] = {R.z[i].x, R.z[i].y, R.z[i].z, R.z[i].w};
+      const float tt[4] = {R.t[i].x, R.t[i].y, R.t[i].z, R.t[i].w};
+      f32x4 rv;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        float phi, dphi;
+        phi_fast<TANH>(zz[u], phi, dphi);
+        rv[u] = ok ? (phi - tt[u]) * dphi : 0.f;
+      }
+      split3(rv, p0, p1, p2);
+      *reinterpret_cast<bf16x4*>(B + o) = p0;
+      *reinterpret_cast<bf16x4*>(B + P::PR + o) = p1;
+      *reinterpret_cast<bf16x4*>(B + 2 * P::PR + o) = p2;
+    }
+  };
+  // transposed fragment reads (k_atr3's lane map)
+  const int gi = lane >> 4, qq = (lane >> 2) & 3, pp = lane & 3;
+  const int frow = 8 * (gi >> 1) + qq, fcol = 16 * (gi & 1) + 4 * pp;
+  auto frag = [&](const __bf16* O, int piece, int cbase, bf16x8 (&f)[3]) {
+    const int o0 = a3_off(frow, cbase + fcol), o1 = a3_off(frow + 4, cbase + fcol);
+#pragma unroll
+    for (int p = 0; p < 3; ++p) {
+      typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
+      const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(O + p * piece + o0));
+      const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(O + p * piece + o1));
+      f[p] = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+    }
+  };
+  const int wr = wave & 1, wc = wave >> 1;   // m half, 64-column quarter
+  f32x16 acc[4][2];
+  zero_acc(acc);
+  auto compute = [&](int st) {
+    const __bf16* A = img + st * P::STAGE;
+    const __bf16* B = A + 3 * P::PA;
+    bf16x8 b[2][3];
+#pragma unroll
+    for (int ni = 0; ni < 2; ++ni) frag(B, P::PR, wc * 64 + ni * 32, b[ni]);
+#pragma unroll
+    for (int mi = 0; mi < 4; ++mi) {
+      bf16x8 a[3];
+      frag(A, P::PA, wr * 128 + mi * 32, a);
+#pragma unroll
+      for (int ni = 0; ni < 2; ++ni) acc[mi][ni] = mfma_split3(a, b[ni], acc[mi][ni]);
+    }
+  };
+  // Measured alternatives (C3, no gain or slower): sched_group_barrier interleaves of the staging
+  // VALU into the MFMA stream (1 MFMA : 3-5 VALU : 1 DS), and the upper four waves staging before
+  // multiplying (opposite phase to their SIMD partner; spills 5 VGPRs).
+  if (r0 < r1) {
+    Atr3wRing R0, R1;
+    gload(R0, r0);
+    gload(R1, r0 + A3_KS);
+    put(0, R0, r0);
+    __syncthreads();
+    for (int64_t k0 = r0; k0 < r1; k0 += 2 * A3_KS) {   // steps in pairs (an odd count ends masked)
+      gload(R0, k0 + 2 * A3_KS);
+      compute(0);
+      put(1, R1, k0 + A3_KS);
+      __syncthreads();
+      gload(R1, k0 + 3 * A3_KS);
+      compute(1);
+      put(0, R0, k0 + 2 * A3_KS);
+      __syncthreads();
+    }
+  }
+  float* out = slab + ((int64_t)sp * 4 + q) * H * H + wc * 64 + (lane & 31);
+#pragma unroll
+  for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int m = wr * 128 + mi * 32 + acc_row(r, lane);
+#pragma unroll
+      for (int ni = 0; ni < 2; ++ni) out[(int64_t)m * H + ni * 32] = acc[mi][ni][r];
+    }
+}
+
+__global__ __launch_bounds__(A3W_THREADS, 1) void k_atr3w(Geom g, const float* __restrict__ Sh,
+                                                         const float* __restrict__ zc, const float* __restrict__ tgt,
+                                                         float* __restrict__ slab, int nsplit) {
+  __shared__ __attribute__((aligned(16))) __bf16 img[2 * A3<256>::STAGE];
+  int lid = xcd_swizzle(blockIdx.x, gridDim.x);
+  const int q = lid % 4;          // the 4 gates of one split share the Hprev rows: same XCD
+  const int sp = lid / 4;
+  const int64_t n = g.BT() * g.H;
+  if (q == 2) atr3w_body<true>(g, q, sp, nsplit, Sh, zc + q * n, tgt + q * n, slab, img);
+  else atr3w_body<false>(g, q, sp, nsplit, Sh, zc + q * n, tgt + q * n, slab, img);
+}
+
 }  // namespace
 
 bool split3_ok(const Geom& g) {   // 32-bit buffer offsets into the h plane and a z-cache plane
@@ -310,10 +446,13 @@ int atr3_splits(const Geom& g) {
   return ns < 1 ? 1 : ns;
 }
 
+bool atr3w_ok(const Geom& g) { return g.H == 256; }
+
 void launch_atr3(const Geom& g, const float* Sh, const float* zc, const float* tgt, float* slab, int nsplit,
-                 hipStream_t s) {
+                 hipStream_t s, bool two_waves) {
   dim3 grid((g.H / A3_BM) * (g.H / A3_BN) * 4 * nsplit);
-  k_atr3<<<grid, kThreads, 0, s>>>(g, Sh, zc, tgt, slab, nsplit);
+  if (two_waves && atr3w_ok(g)) k_atr3w<<<4 * nsplit, A3W_THREADS, 0, s>>>(g, Sh, zc, tgt, slab, nsplit);
+  else k_atr3<<<grid, kThreads, 0, s>>>(g, Sh, zc, tgt, slab, nsplit);
 }
 
 void launch_split_g(const Geom& g, const float* G, float* gimg, hipStream_t s) {

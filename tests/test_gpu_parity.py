@@ -817,6 +817,36 @@ def test_q_two_piece_split_same_trajectory(shape, mods, dev, monkeypatch):
     assert torch.equal(out[0][1], out[1][1])
 
 
+@pytest.mark.parametrize('shape', [(2048, 8, 16, 256), (333, 3, 5, 256)])
+def test_atr3_two_waves_bit_identical(shape, mods, dev, monkeypatch):
+    """k_atr3w (8 waves, two per SIMD, the default at H = 256) forms the h-side gradient slabs with
+    the same products in the same order as k_atr3 (ADMM_ATR3W=0, one wave per SIMD): trajectories
+    must be bitwise equal, including a ragged row split (B*T not a multiple of 16)."""
+    from blocks.lstm import LSTM
+    from parameters import example_parameter_dictionary
+    admm, _ = mods
+    admm.with_dual_y = False
+    B, T, D, H = shape
+    g = torch.Generator().manual_seed(23)
+    x = torch.rand(B, T, D, generator=g).to(dev)
+    y = (0.8 * x.mean((1, 2)).unsqueeze(1) + 0.1 * torch.rand(B, 1, generator=g).to(dev)).contiguous()
+    out = []
+    for mode in ('0', '1'):
+        monkeypatch.setenv('ADMM_ATR3W', mode)
+        torch.manual_seed(0)
+        m = LSTM(D, H, 1).to(dev)
+        opt = admm.ADMMBasedOptimizer(m, (x, y), example_parameter_dictionary['GoogleStock'], verbose=False)
+        ks = []
+        for _ in range(4):
+            opt.step()
+            ks.append(list(opt.last_step_stats()['k'].values()))
+        out.append((ks, torch.cat([p.detach().flatten() for p in m.parameters()]
+                                  + [v.flatten() for v in opt.gates.values()])))
+        del opt
+    assert out[0][0] == out[1][0]
+    assert torch.equal(out[0][1], out[1][1])
+
+
 def test_generic_weight_stage_matches_fast(mods, dev, monkeypatch):
     """ADMM_GENERIC=1 runs the weight stages on the generic kernels (materialised R and Q, f32 MFMA
     GEMMs) instead of the fast streaming path.  Step 1 decides identically on both: the x-side

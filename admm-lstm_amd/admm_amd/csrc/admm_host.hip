@@ -122,7 +122,9 @@ struct AdmmCtx {
   // enters the line-search increments, where 2^-16 relative is far inside the reference's own
   // rounding of W + G/theta (DESIGN.md "trial direction precision"); G itself stays split3.
   int q_pieces = 2;
-  bool atr3w = true;       // k_atr3w (two waves per SIMD) for the h-side gradient; ADMM_ATR3W=0: k_atr3
+  bool atr3w = true;
+  // Q in the row-pair layout (k_qgemm3 -> k_trial_rows<1>; ADMM_QPAIR=0: row-major)
+  bool qpair = true;       // k_atr3w (two waves per SIMD) for the h-side gradient; ADMM_ATR3W=0: k_atr3
   float* gimg = nullptr;   // split image of G_h for k_qgemm3
   hipStream_t sx[kMaxSweepStreams - 1] = {};
   hipEvent_t ev_fork = nullptr, ev_join[kMaxSweepStreams - 1] = {};
@@ -300,7 +302,7 @@ int stage_weights(AdmmCtx* c, int side, hipStream_t s) {
   // 2. trial direction Q = A G (not needed on the fast x side: formed inside the trials)
   if (!(fast && side == 0)) {
     ProfScope ps(c, side == 0 ? ADMM_PROF_QGEMM_X : ADMM_PROF_QGEMM_H, s);
-    if (side == 1 && c->split3) launch_qgemm3(g, c->buf.gates[ADMM_H], c->G, c->gimg, c->Q, s, c->q_pieces);
+    if (side == 1 && c->split3) launch_qgemm3(g, c->buf.gates[ADMM_H], c->G, c->gimg, c->Q, s, c->q_pieces, c->qpair);
     else launch_qgemm(g, side, c->buf.x, c->buf.gates[ADMM_H], c->G, c->Q, s);
   }
   // 3. line search: trial passes of kTrialJ exponents each until every gate has passed
@@ -331,7 +333,8 @@ int stage_weights(AdmmCtx* c, int side, hipStream_t s) {
       }
       if (fast)
         launch_trial_fast(g, side, pass, side == 1 ? zh : c->zc, c->tgt, side == 1 ? c->Q : nullptr, c->buf.x,
-                          side == 0 ? c->G : c->dW, c->found, c->tr_part, nblk, s, sx.zx ? &sx : nullptr);
+                          side == 0 ? c->G : c->dW, c->found, c->tr_part, nblk, s, sx.zx ? &sx : nullptr,
+                          side == 1 && c->split3 && c->qpair);
       else
         launch_trial(g, pass, c->zc, c->tgt, c->Q, c->found, c->tr_part, nblk, s);
     }
@@ -462,6 +465,7 @@ int admm_create(const AdmmDims* dims, const AdmmParams* params, int device, Admm
   if (const char* e = std::getenv("ADMM_SPEC_X")) c->spec_x = c->spec_x && std::atoi(e) != 0;
   if (const char* e = std::getenv("ADMM_SPLIT3")) c->split3 = c->split3 && std::atoi(e) != 0;
   if (const char* e = std::getenv("ADMM_ATR3W")) c->atr3w = std::atoi(e) != 0;
+  if (const char* e = std::getenv("ADMM_QPAIR")) c->qpair = std::atoi(e) != 0;
   if (const char* e = std::getenv("ADMM_Q_PIECES")) c->q_pieces = std::atoi(e) == 2 ? 2 : 3;
   Hyper& h = c->hp;
   for (int i = 0; i < 7; ++i) h.rho[i] = params->rho[i];

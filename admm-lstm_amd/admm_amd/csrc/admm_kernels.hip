@@ -1583,8 +1583,9 @@ __global__ __launch_bounds__(kThreads, TF_MINB) void k_trial_fast(Geom g, int pa
 // are wave-uniform (scalar loads, SGPR operands) and the thread's column of G_x stays in 16
 // VGPRs for the whole pass: q = x_row . G_x costs 16 FMAs and no LDS.  The two rows are the two
 // halves of trial_pair's packed arithmetic; the next pair's operands are loaded while this one
-// is evaluated.  Side 1 reads q from Q instead.
-template <bool TANH, int SIDE, int DP, bool XV, bool SPEC>
+// is evaluated.  Side 1 reads q from Q instead (QP: Q in k_qgemm3's row-pair layout
+// [row / 2][j][row % 2], one float2 per pair).
+template <bool TANH, int SIDE, int DP, bool XV, bool SPEC, bool QP = false>
 __device__ __forceinline__ void trial_rows_body(const Geom& g, int q, int pass, const float* __restrict__ zc,
                                                 const float* __restrict__ tgt, const float* __restrict__ Q,
                                                 const float* __restrict__ x, const float* __restrict__ Gx, int blk,
@@ -1594,7 +1595,7 @@ __device__ __forceinline__ void trial_rows_body(const Geom& g, int q, int pass, 
   const int j = blockIdx.z * 256 + threadIdx.x;
   const float* __restrict__ zq = zc + (int64_t)q * n + j;
   const float* __restrict__ tq = tgt + (int64_t)q * n + j;
-  const float* __restrict__ Qq = Q ? Q + (int64_t)q * n + j : nullptr;
+  const float* __restrict__ Qq = Q ? Q + (int64_t)q * n + (QP ? 2 * j : j) : nullptr;
   float gw[DP];
 #pragma unroll
   for (int d = 0; d < DP; ++d) gw[d] = (SIDE == 0 && d < g.D) ? Gx[((int64_t)q * g.D + d) * g.H + j] : 0.f;
@@ -1625,6 +1626,9 @@ __device__ __forceinline__ void trial_rows_body(const Geom& g, int q, int pass, 
     if (SIDE == 0) {
       load_xrow<DP, XV>(x, r0, g.D, v.xa);
       load_xrow<DP, XV>(x, r1, g.D, v.xb);
+    } else if constexpr (QP) {   // ra is even and BT is even: rows ra, ra + 1 are one pair
+      const int64_t pr = __builtin_amdgcn_readfirstlane((int)((ra < BT ? ra : BT - 2) >> 1));
+      v.q = __builtin_nontemporal_load(reinterpret_cast<const f32x2*>(Qq + pr * 2 * g.H));
     } else {
       v.q = f32x2{__builtin_nontemporal_load(Qq + r0 * g.H), __builtin_nontemporal_load(Qq + r1 * g.H)};
     }
@@ -1680,7 +1684,7 @@ __device__ __forceinline__ void trial_rows_body(const Geom& g, int q, int pass, 
   dq_run(dq, acc, true);
 }
 
-template <int SIDE, int DP, bool XV, bool SPEC>
+template <int SIDE, int DP, bool XV, bool SPEC, bool QP = false>
 __global__ __launch_bounds__(kThreads) void k_trial_rows(Geom g, int pass, const float* __restrict__ zc,
                                                          const float* __restrict__ tgt, const float* __restrict__ Q,
                                                          const float* __restrict__ x, const float* __restrict__ Gx,
@@ -1694,8 +1698,8 @@ __global__ __launch_bounds__(kThreads) void k_trial_rows(Geom g, int pass, const
   __shared__ float dqbuf[kThreads / 64][5 * kDQ];
   __shared__ float4 dwl[SPEC ? DP / 4 * 256 : 1];
   DirectQ dq{dqbuf[threadIdx.x >> 6], 0, 0};
-  if (q == 2) trial_rows_body<true, SIDE, DP, XV, SPEC>(g, q, pass, zc, tgt, Q, x, Gx, blk, nblk, acc, dq, sp, dwl);
-  else trial_rows_body<false, SIDE, DP, XV, SPEC>(g, q, pass, zc, tgt, Q, x, Gx, blk, nblk, acc, dq, sp, dwl);
+  if (q == 2) trial_rows_body<true, SIDE, DP, XV, SPEC, QP>(g, q, pass, zc, tgt, Q, x, Gx, blk, nblk, acc, dq, sp, dwl);
+  else trial_rows_body<false, SIDE, DP, XV, SPEC, QP>(g, q, pass, zc, tgt, Q, x, Gx, blk, nblk, acc, dq, sp, dwl);
   // the column blocks of one (blk, q) add into the same part slot row: blk index widened by z
   trial_block_store(acc, part, q, blockIdx.z * nblk + blk, nblk * gridDim.z);
 }
@@ -2617,12 +2621,15 @@ bool trial_mx_ok(const Geom& g) {   // ADMM_TRIAL_MX=0: the x side on k_trial_ro
 
 void launch_trial_fast(const Geom& g, int side, int pass, const float* zc, const float* tgt, const float* Q,
                        const float* x, const float* Wsrc, const int* found, double* part, int nblk, hipStream_t s,
-                       const SpecX* spec) {
+                       const SpecX* spec, bool qpair) {
   dim3 grid(nblk, 4);
   const SpecX sp = spec ? *spec : SpecX{};
   if (side == 1 && trial_rows_ok(g)) {
     dim3 gr(nblk, 4, g.H / 256);
-    k_trial_rows<1, 4, false, false><<<gr, kThreads, 0, s>>>(g, pass, zc, tgt, Q, x, Wsrc, found, part, nblk, sp);
+    if (qpair && qpair_ok(g))
+      k_trial_rows<1, 4, false, false, true><<<gr, kThreads, 0, s>>>(g, pass, zc, tgt, Q, x, Wsrc, found, part, nblk, sp);
+    else
+      k_trial_rows<1, 4, false, false><<<gr, kThreads, 0, s>>>(g, pass, zc, tgt, Q, x, Wsrc, found, part, nblk, sp);
     return;
   }
   if (side == 1) {  // no x . W product on this side: one instantiation

@@ -171,7 +171,7 @@ struct SpecX {
 };
 void launch_trial_fast(const Geom& g, int side, int pass, const float* zc, const float* tgt, const float* Q,
                        const float* x, const float* Wsrc, const int* found, double* part, int nblk, hipStream_t s,
-                       const SpecX* spec = nullptr);
+                       const SpecX* spec = nullptr, bool qpair = false);
 // after the x decision: zx = zc + X dWx for the gates whose exponent was mispredicted
 void launch_apply_fix(const Geom& g, const float* x, const float* dW, const float* zc, float* zx, const int* kpred,
                       const DevStats* stats, hipStream_t s);
@@ -201,12 +201,15 @@ void launch_atr3(const Geom& g, const float* Sh, const float* zc, const float* t
                  hipStream_t s, bool two_waves = true);
 // pieces = 3: f32-accurate split3 products; 2: two-way splits, three products (~2^-16 relative),
 // enough for the trial direction ("trial direction precision")
+// qpair (and qpair_ok: BT even): Q in the row-pair layout [q][row / 2][j][row % 2] that
+// launch_trial_fast(..., qpair = true) reads (the h-side trial pass, H % 256 == 0)
+bool qpair_ok(const Geom& g);
 void launch_qgemm3(const Geom& g, const float* Sh, const float* G, float* gimg, float* Q, hipStream_t s,
-                   int pieces = 3);
+                   int pieces = 3, bool qpair = false);
 // the two halves of launch_qgemm3: G -> split image, then Q = Hprev G (gates with found[q] set skipped)
 void launch_split_g(const Geom& g, const float* G, float* gimg, hipStream_t s);
 void launch_qgemm3_img(const Geom& g, const float* Sh, const float* gimg, float* Q, const int* found, hipStream_t s,
-                       int pieces = 3);
+                       int pieces = 3, bool qpair = false);
 // decide the first passing k in this pass's window; on success update the weights
 struct SelectArgs {
   int side;                 // 0 x, 1 h

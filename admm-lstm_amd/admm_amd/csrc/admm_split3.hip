@@ -49,7 +49,11 @@ __global__ __launch_bounds__(kThreads) void k_split_g(int H, const float* __rest
 // One 128 x 256 tile of one gate per workgroup (qgemm3_tile).  found != nullptr: gates whose
 // line search has already decided are skipped (the later trial passes, when pass 0 ran fused
 // in k_qtrial3 and Q was never formed).
-template <int NP>
+// QP: Q is written in the row-pair layout Q[q][row / 2][j][row % 2] (BT even): registers r and
+// r + 1 of a 32x32 accumulator hold rows 2i, 2i + 1 of one column, so each lane stores 8 B and a
+// wave-instruction two contiguous 256-B runs -- half the store instructions of the row-major
+// layout (the epilogue is store-issue bound); the h-side trial reads a row pair as one float2.
+template <int NP, bool QP>
 __global__ __launch_bounds__(kThreads) void k_qgemm3(Geom g, const float* __restrict__ Sh,
                                                       const bf16x8* __restrict__ gi, float* __restrict__ Q,
                                                       const int* __restrict__ found) {
@@ -65,6 +69,21 @@ __global__ __launch_bounds__(kThreads) void k_qgemm3(Geom g, const float* __rest
   qgemm3_tile<NP>(g, Sh, gi, q, cb, m0, lds, acc);
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, wr = wave >> 1, wc = wave & 1, c32 = lane & 31;
   float* Qq = Q + (int64_t)q * BT * H + Q3_BN * cb + wc * 128 + c32;
+  if constexpr (QP) {
+    typedef float f32x2 __attribute__((ext_vector_type(2)));
+    f32x2* Qp = reinterpret_cast<f32x2*>(Q + (int64_t)q * BT * H) + Q3_BN * cb + wc * 128 + c32;
+#pragma unroll
+    for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+      for (int r = 0; r < 16; r += 2) {
+        const int64_t row = m0 + wr * 64 + mi * 32 + acc_row(r, lane);   // even
+        if (row >= BT) continue;
+#pragma unroll
+        for (int ni = 0; ni < 4; ++ni)
+          __builtin_nontemporal_store(f32x2{acc[mi][ni][r], acc[mi][ni][r + 1]}, Qp + (row >> 1) * H + ni * 32);
+      }
+    return;
+  }
 #pragma unroll
   for (int mi = 0; mi < 2; ++mi)
 #pragma unroll
@@ -460,17 +479,24 @@ void launch_split_g(const Geom& g, const float* G, float* gimg, hipStream_t s) {
   k_split_g<<<(total + kThreads - 1) / kThreads, kThreads, 0, s>>>(g.H, G, reinterpret_cast<bf16x8*>(gimg));
 }
 
+bool qpair_ok(const Geom& g) { return g.BT() % 2 == 0; }
+
 void launch_qgemm3_img(const Geom& g, const float* Sh, const float* gimg, float* Q, const int* found, hipStream_t s,
-                       int pieces) {
+                       int pieces, bool qpair) {
   const int64_t nrt = (g.BT() + Q3_BM - 1) / Q3_BM;
   dim3 grid((unsigned)(nrt * 4 * (g.H / Q3_BN)));
-  if (pieces == 2) k_qgemm3<2><<<grid, kThreads, 0, s>>>(g, Sh, reinterpret_cast<const bf16x8*>(gimg), Q, found);
-  else k_qgemm3<3><<<grid, kThreads, 0, s>>>(g, Sh, reinterpret_cast<const bf16x8*>(gimg), Q, found);
+  const bf16x8* gb = reinterpret_cast<const bf16x8*>(gimg);
+  qpair = qpair && qpair_ok(g);
+  if (pieces == 2 && qpair) k_qgemm3<2, true><<<grid, kThreads, 0, s>>>(g, Sh, gb, Q, found);
+  else if (pieces == 2) k_qgemm3<2, false><<<grid, kThreads, 0, s>>>(g, Sh, gb, Q, found);
+  else if (qpair) k_qgemm3<3, true><<<grid, kThreads, 0, s>>>(g, Sh, gb, Q, found);
+  else k_qgemm3<3, false><<<grid, kThreads, 0, s>>>(g, Sh, gb, Q, found);
 }
 
-void launch_qgemm3(const Geom& g, const float* Sh, const float* G, float* gimg, float* Q, hipStream_t s, int pieces) {
+void launch_qgemm3(const Geom& g, const float* Sh, const float* G, float* gimg, float* Q, hipStream_t s, int pieces,
+                   bool qpair) {
   launch_split_g(g, G, gimg, s);
-  launch_qgemm3_img(g, Sh, gimg, Q, nullptr, s, pieces);
+  launch_qgemm3_img(g, Sh, gimg, Q, nullptr, s, pieces, qpair);
 }
 
 }  // namespace admm

@@ -69,7 +69,9 @@ template <int NP>
 __device__ __forceinline__ void qgemm3_tile(const Geom& g, const float* __restrict__ Sh,
                                             const bf16x8* __restrict__ gi, int q, int cb, int64_t m0,
                                             char* lds, f32x16 (&acc)[2][4]) {
-  constexpr int AP = kQ3AP, BU = kQ3BU;
+  // B image per step: NP = 3 all three pieces of each 32-column tile (192 units), NP = 2 only
+  // pieces 0 and 1 (128 units): the third piece is never multiplied there
+  constexpr int AP = kQ3AP, PSTR = NP == 3 ? 192 : 128, BU = (Q3_BN / 32) * PSTR;
   __bf16* As = reinterpret_cast<__bf16*>(lds);                       // [2][3 * AP]
   bf16x8* Bs = reinterpret_cast<bf16x8*>(lds + 2 * 3 * AP * 2);       // [2][BU]
   const int H = g.H, NK = H / 16, NTT = H / 32;
@@ -81,32 +83,31 @@ __device__ __forceinline__ void qgemm3_tile(const Geom& g, const float* __restri
   const float* ap = Sh + g.hrow(arow) * H + 8 * sh;
   const bf16x8* bp = gi + ((size_t)q * NK * NTT + (size_t)(Q3_BN / 32) * cb) * 192 + tid;
   const size_t bstep = (size_t)NTT * 192;
-  float4 ra0, ra1;
-  bf16x8 rb[BU / kThreads];
-  auto gload = [&](int c) {
+  // two-slot register ring: the loads of step c + 2 are issued at step c (one step of MFMAs does
+  // not cover the L2/HBM latency of the next operands); NK is even (H % 256 == 0)
+  struct Slot { float4 a0, a1; bf16x8 b[BU / kThreads]; };
+  auto gload = [&](Slot& r, int c) {
+    if (c >= NK) return;
     if (S3_ABL & 32) {
-      ra0 = make_float4(c, 1.f, 2.f, 3.f); ra1 = ra0;
+      r.a0 = make_float4(c, 1.f, 2.f, 3.f); r.a1 = r.a0;
     } else {
-      ra0 = *reinterpret_cast<const float4*>(ap + 16 * c);
-      ra1 = *reinterpret_cast<const float4*>(ap + 16 * c + 4);
+      r.a0 = *reinterpret_cast<const float4*>(ap + 16 * c);
+      r.a1 = *reinterpret_cast<const float4*>(ap + 16 * c + 4);
     }
 #pragma unroll
-    for (int u = 0; u < BU / kThreads; ++u) rb[u] = bp[c * bstep + u * kThreads];
+    for (int u = 0; u < BU / kThreads; ++u) {
+      const int i = tid + u * kThreads;   // image unit -> G-image unit (skipping piece 2 for NP = 2)
+      const int src = NP == 3 ? i : (i >> 7) * 192 + (i & 127);
+      r.b[u] = bp[c * bstep + src - tid];
+    }
   };
-  auto lstore = [&](int st) {
-    put3<NP>(As + st * 3 * AP, AP, sw_off(sr, sh), f32x8{ra0.x, ra0.y, ra0.z, ra0.w, ra1.x, ra1.y, ra1.z, ra1.w});
+  auto lstore = [&](int st, const Slot& r) {
+    put3<NP>(As + st * 3 * AP, AP, sw_off(sr, sh), f32x8{r.a0.x, r.a0.y, r.a0.z, r.a0.w, r.a1.x, r.a1.y, r.a1.z, r.a1.w});
 #pragma unroll
-    for (int u = 0; u < BU / kThreads; ++u) Bs[st * BU + tid + u * kThreads] = rb[u];
+    for (int u = 0; u < BU / kThreads; ++u) Bs[st * BU + tid + u * kThreads] = r.b[u];
   };
   const int wr = wave >> 1, wc = wave & 1, c32 = lane & 31, kh = lane >> 5;
-  zero_acc(acc);
-  gload(0);
-  lstore(0);
-  __syncthreads();
-  for (int c = 0; c < NK; ++c) {
-    const int st = c & 1;
-    if (c + 1 < NK) gload(c + 1);
-    __builtin_amdgcn_sched_barrier(0);
+  auto compute = [&](int st) {
 #pragma unroll
     for (int mi = 0; mi < 2; ++mi) {
       bf16x8 a[3];
@@ -119,15 +120,32 @@ __device__ __forceinline__ void qgemm3_tile(const Geom& g, const float* __restri
       }
 #pragma unroll
       for (int ni = 0; ni < 4; ++ni) {
-        const bf16x8* bb = &Bs[st * BU + (wc * 4 + ni) * 192 + lane];
+        const bf16x8* bb = &Bs[st * BU + (wc * 4 + ni) * PSTR + lane];
         const bf16x8 b[3] = {bb[0], bb[64], NP == 3 ? bb[128] : bb[0]};
         if (S3_ABL & 64) acc[mi][ni][0] += (float)a[0][0] * (float)b[0][0];
         else if (NP == 3) acc[mi][ni] = mfma_split3(a, b, acc[mi][ni]);
         else acc[mi][ni] = mfma_split2(a, b, acc[mi][ni]);
       }
     }
+  };
+  zero_acc(acc);
+  Slot R0, R1;
+  gload(R0, 0);
+  gload(R1, 1);
+  lstore(0, R0);
+  __syncthreads();
+  for (int c = 0; c < NK; c += 2) {
+    gload(R0, c + 2);
     __builtin_amdgcn_sched_barrier(0);
-    if (c + 1 < NK) lstore(st ^ 1);
+    compute(0);
+    __builtin_amdgcn_sched_barrier(0);
+    lstore(1, R1);
+    __syncthreads();
+    gload(R1, c + 3);
+    __builtin_amdgcn_sched_barrier(0);
+    compute(1);
+    __builtin_amdgcn_sched_barrier(0);
+    if (c + 2 < NK) lstore(0, R0);
     __syncthreads();
   }
 }

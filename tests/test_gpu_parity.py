@@ -817,11 +817,14 @@ def test_q_two_piece_split_same_trajectory(shape, mods, dev, monkeypatch):
     assert torch.equal(out[0][1], out[1][1])
 
 
-@pytest.mark.parametrize('shape', [(2048, 8, 16, 256), (333, 3, 5, 256)])
-def test_atr3_two_waves_bit_identical(shape, mods, dev, monkeypatch):
-    """k_atr3w (8 waves, two per SIMD, the default at H = 256) forms the h-side gradient slabs with
-    the same products in the same order as k_atr3 (ADMM_ATR3W=0, one wave per SIMD): trajectories
-    must be bitwise equal, including a ragged row split (B*T not a multiple of 16)."""
+@pytest.mark.parametrize('knob,shape', [('ADMM_ATR3W', (2048, 8, 16, 256)), ('ADMM_ATR3W', (333, 3, 5, 256)),
+                                        ('ADMM_QPAIR', (1000, 5, 16, 256)), ('ADMM_QPAIR', (301, 3, 16, 512))])
+def test_h_stage_layout_knobs_bit_identical(knob, shape, mods, dev, monkeypatch):
+    """ADMM_ATR3W: k_atr3w (8 waves, two per SIMD, the default at H = 256) forms the h-side
+    gradient slabs with the same products in the same order as k_atr3 (one wave per SIMD).
+    ADMM_QPAIR: k_qgemm3 stores Q in the row-pair layout that the h-side trials read (default)
+    instead of row-major (the same values).  Either way the trajectories must be bitwise equal,
+    including a ragged row split (B*T not a multiple of 16) and odd B*T (row-major fallback)."""
     from blocks.lstm import LSTM
     from parameters import example_parameter_dictionary
     admm, _ = mods
@@ -832,7 +835,7 @@ def test_atr3_two_waves_bit_identical(shape, mods, dev, monkeypatch):
     y = (0.8 * x.mean((1, 2)).unsqueeze(1) + 0.1 * torch.rand(B, 1, generator=g).to(dev)).contiguous()
     out = []
     for mode in ('0', '1'):
-        monkeypatch.setenv('ADMM_ATR3W', mode)
+        monkeypatch.setenv(knob, mode)
         torch.manual_seed(0)
         m = LSTM(D, H, 1).to(dev)
         opt = admm.ADMMBasedOptimizer(m, (x, y), example_parameter_dictionary['GoogleStock'], verbose=False)

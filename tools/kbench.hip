@@ -78,8 +78,12 @@ int main(int argc, char** argv) {
     float* Q3; (void)hipMalloc(&Q3, (size_t)4 * n * 4);
     timeit("atr3 (split bf16)", f4 * (2 * 4 * n + BT * g.H), 2.0 * BT * g.H * 4 * g.H,
            [&] { launch_atr3(g, S.p[5], zc, tgt, slab3, ns3, s); });
+    timeit("atr3 (1 wave/SIMD)", f4 * (2 * 4 * n + BT * g.H), 2.0 * BT * g.H * 4 * g.H,
+           [&] { launch_atr3(g, S.p[5], zc, tgt, slab3, ns3, s, false); });
     timeit("qgemm3 (split bf16)", f4 * (4 * n + BT * g.H), 2.0 * BT * g.H * 4 * g.H,
            [&] { launch_qgemm3(g, S.p[5], G, gimg, Q3, s); });
+    timeit("qgemm3 (2 pieces)", f4 * (4 * n + BT * g.H), 2.0 * BT * g.H * 4 * g.H,
+           [&] { launch_qgemm3(g, S.p[5], G, gimg, Q3, s, 2); });
     launch_atr_fused(g, hp, x, S.p[5], zc, tgt, dW, slab, atr_splits(g, 1), s);
     launch_qgemm(g, 1, x, S.p[5], G, Q, s);
     (void)hipDeviceSynchronize();
@@ -128,7 +132,7 @@ int main(int argc, char** argv) {
          [&] { launch_atr(g, 1, x, S.p[5], R, slab, ns, s); });
   timeit("qgemm side1", f4 * (4 * n + BT * g.H), 2.0 * BT * g.H * 4 * g.H, [&] { launch_qgemm(g, 1, x, S.p[5], G, Q, s); });
   run_s3();
-  SweepT sw{x, S, L, zc, nullptr, 0, g.B};
+  SweepT sw{x, S, L, zc, nullptr, nullptr, nullptr, 0, g.B};
   timeit("sweep_t (t=5)", f4 * g.B * (g.D + 27.0 * g.H), 2.0 * g.B * (g.D + g.H) * 4 * g.H,
          [&] { launch_sweep_t(g, 5, w, hp, sw, s); });
   {

@@ -1939,27 +1939,58 @@ __global__ __launch_bounds__(kThreads) void k_resid_gx(Geom g, Hyper hp, const f
   for (int i = threadIdx.x; i < g.D * g.H; i += kThreads) out[i] = gl[i];
 }
 
+// the fast kernels' arithmetic (trial_pair: polynomial regime and per-candidate queue) over
+// element pairs
+template <bool TANH>
+__device__ __forceinline__ void trial_pair_loop(int64_t n, const float* z, const float* tgt, const float* qv, int pass,
+                                                int blk, int nblk, float (&acc)[kSlots], DirectQ& dq) {
+  f32x2 acc2[kPair];
+#pragma unroll
+  for (int k = 0; k < kPair; ++k) acc2[k] = f32x2{0.f, 0.f};
+  const int64_t np = (n + 1) / 2;
+  for (int64_t base = (int64_t)blk * kThreads; base < np; base += (int64_t)nblk * kThreads) {   // wave-uniform
+    const int64_t v = base + threadIdx.x;
+    const bool ok = v < np, oky = 2 * v + 1 < n;
+    const f32x2 zz = f32x2{ok ? z[2 * v] : 0.f, oky ? z[2 * v + 1] : 0.f};
+    const f32x2 tt = f32x2{ok ? tgt[2 * v] : 0.f, oky ? tgt[2 * v + 1] : 0.f};
+    const f32x2 qq = f32x2{ok ? qv[2 * v] : 0.f, oky ? qv[2 * v + 1] : 0.f};
+    trial_pair<TANH>(ok, zz, tt, qq, pass, acc, acc2, dq, oky);
+    dq_run(dq, acc, false);
+  }
+  trial_pair_fold(acc, acc2);
+  dq_run(dq, acc, true);
+}
+
 // Test hook: the same per-element arithmetic on caller data (one gate), kbase = pass*J:
-// per block the J candidate sums of that window, with the polynomial part already
-// evaluated at s = 2^-(kbase+k), so part[blk][k] is the full increment sum.
-__global__ __launch_bounds__(kThreads) void k_trial_debug(int64_t n, int tanh_gate, int kbase, const float* z,
+// per block the J candidate sums of that window, with the polynomial part already evaluated at
+// s = 2^-(kbase+k), so part[blk][k] is the full increment sum.  mode bit 0: tanh gate; bit 1:
+// the fast kernels' pair arithmetic (trial_pair) instead of the generic trial_point.
+__global__ __launch_bounds__(kThreads) void k_trial_debug(int64_t n, int mode, int kbase, const float* z,
                                                             const float* tgt, const float* qv, double* part) {
   __shared__ double red[4][kSlots];
   float acc[kSlots];
 #pragma unroll
   for (int k = 0; k < kSlots; ++k) acc[k] = 0.f;
   const int pass = kbase / kTrialJ;
+  const bool tanh_gate = mode & 1, pair = mode & 2;
   // the polynomial slots are only filled on pass 0: run pass 0 for them, then this pass
   __shared__ float dqbuf[kThreads / 64][5 * kDQ];
   DirectQ dq{dqbuf[threadIdx.x >> 6], 0, 0};
-  if (tanh_gate) trial_loop<true, 1>(n, z, tgt, qv, 0, blockIdx.x, gridDim.x, acc, dq);
-  else trial_loop<false, 1>(n, z, tgt, qv, 0, blockIdx.x, gridDim.x, acc, dq);
+  auto run = [&](int ps, float (&a)[kSlots]) {
+    if (pair) {
+      if (tanh_gate) trial_pair_loop<true>(n, z, tgt, qv, ps, blockIdx.x, gridDim.x, a, dq);
+      else trial_pair_loop<false>(n, z, tgt, qv, ps, blockIdx.x, gridDim.x, a, dq);
+    } else {
+      if (tanh_gate) trial_loop<true, 1>(n, z, tgt, qv, ps, blockIdx.x, gridDim.x, a, dq);
+      else trial_loop<false, 1>(n, z, tgt, qv, ps, blockIdx.x, gridDim.x, a, dq);
+    }
+  };
+  run(0, acc);
   if (pass > 0) {
     float acc2[kSlots];
 #pragma unroll
     for (int k = 0; k < kSlots; ++k) acc2[k] = 0.f;
-    if (tanh_gate) trial_loop<true, 1>(n, z, tgt, qv, pass, blockIdx.x, gridDim.x, acc2, dq);
-    else trial_loop<false, 1>(n, z, tgt, qv, pass, blockIdx.x, gridDim.x, acc2, dq);
+    run(pass, acc2);
 #pragma unroll
     for (int k = 0; k < kTrialJ; ++k) acc[k] = acc2[k];
   }

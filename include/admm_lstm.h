@@ -174,7 +174,9 @@ int admm_profile_read(AdmmCtx* ctx, double* ms /* [ADMM_PROF_CLASSES] */, int32_
 
 /* Test hook (synchronous): the line-search trial arithmetic of one gate on caller data.
    out[k] (host, 16 doubles) = sum_e [(phi(z_e + q_e 2^-(kbase+k)) - tgt_e)^2 - (phi(z_e) - tgt_e)^2],
-   phi = tanh if tanh_gate else sigmoid (the increment form of admm.py:316-334). */
+   phi = tanh if (tanh_gate & 1) else sigmoid (the increment form of admm.py:316-334).
+   tanh_gate & 2: with the fast kernels' packed pair arithmetic instead of the generic kernels'
+   per-element one. */
 int admm_debug_trial(const float* z, const float* tgt, const float* q, int64_t n, int32_t tanh_gate, int32_t kbase,
                      double* out, void* stream);
 

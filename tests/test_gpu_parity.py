@@ -236,9 +236,11 @@ def test_line_search_matches_fp64_oracle(shape, variant, mods, dev):
     assert sum(k > 0 for k, _ in ref) >= 4, ref   # the searches actually iterate
 
 
+@pytest.mark.parametrize('pair', [0, 2])
 @pytest.mark.parametrize('tanh_gate', [0, 1])
-def test_trial_increments_vs_fp64(tanh_gate, dev):
-    """The trial-pass arithmetic: sum_e [(phi(z+q 2^-k)-t)^2 - (phi(z)-t)^2] vs numpy fp64."""
+def test_trial_increments_vs_fp64(tanh_gate, pair, dev):
+    """The trial-pass arithmetic: sum_e [(phi(z+q 2^-k)-t)^2 - (phi(z)-t)^2] vs numpy fp64, for the
+    generic kernels' per-element form and (pair = 2) the fast kernels' packed pair form."""
     from admm_amd import _native as N
     lib = N.load()
     rng = np.random.default_rng(5)
@@ -253,7 +255,7 @@ def test_trial_increments_vs_fp64(tanh_gate, dev):
     d0 = phi(z64) - t64
     for kbase in (0, 16):
         out = (ctypes.c_double * 16)()
-        N.check(lib.admm_debug_trial(N.ptr(zt), N.ptr(tt), N.ptr(qt), n, tanh_gate, kbase, out,
+        N.check(lib.admm_debug_trial(N.ptr(zt), N.ptr(tt), N.ptr(qt), n, tanh_gate | pair, kbase, out,
                                      N.stream_handle(dev)), 'admm_debug_trial')
         for k in range(16):
             kk = kbase + k
@@ -264,8 +266,9 @@ def test_trial_increments_vs_fp64(tanh_gate, dev):
             assert abs(out[k] - ref) <= 2e-5 * scale + 1e-30, (kk, out[k], ref, scale)
 
 
+@pytest.mark.parametrize('pair', [0, 2])
 @pytest.mark.parametrize('tanh_gate', [0, 1])
-def test_trial_polynomial_band_vs_fp64(tanh_gate, dev):
+def test_trial_polynomial_band_vs_fp64(tanh_gate, pair, dev):
     """Elements at the top of the polynomial regime (|q| in [2^-9, 2^-5]: 5-term Taylor in s,
     admm_kernels.hpp kPolyQ), every exponent of the first two windows, vs numpy fp64."""
     from admm_amd import _native as N
@@ -281,7 +284,7 @@ def test_trial_polynomial_band_vs_fp64(tanh_gate, dev):
     d0 = phi(z64) - t64
     for kbase in (0, 16):
         out = (ctypes.c_double * 16)()
-        N.check(lib.admm_debug_trial(N.ptr(zt), N.ptr(tt), N.ptr(qt), n, tanh_gate, kbase, out,
+        N.check(lib.admm_debug_trial(N.ptr(zt), N.ptr(tt), N.ptr(qt), n, tanh_gate | pair, kbase, out,
                                      N.stream_handle(dev)), 'admm_debug_trial')
         for k in range(16):
             kk = kbase + k

@@ -314,7 +314,7 @@ int stage_weights(AdmmCtx* c, int side, hipStream_t s) {
   sa.G = c->G;
   for (int q = 0; q < 4; ++q) sa.W[q] = side == 0 ? c->buf.wx[q] : c->buf.wh[q];
   sa.dW = side == 0 ? c->dW : nullptr;
-  sa.found = c->found;
+  const bool fused_reduce = !c->comm && !c->host_ar;   // one process: k_select reduces the partials
   sa.pick = c->pick;
   sa.stats = c->stats;
   const int nblk = fast ? stream_blocks(g) : c->nblk_trial;
@@ -333,15 +333,23 @@ int stage_weights(AdmmCtx* c, int side, hipStream_t s) {
       }
       if (fast)
         launch_trial_fast(g, side, pass, side == 1 ? zh : c->zc, c->tgt, side == 1 ? c->Q : nullptr, c->buf.x,
-                          side == 0 ? c->G : c->dW, c->found, c->tr_part, nblk, s, sx.zx ? &sx : nullptr,
+                          side == 0 ? c->G : c->dW, c->found + 4 * (pass & 1), c->tr_part, nblk, s, sx.zx ? &sx : nullptr,
                           side == 1 && c->split3 && c->qpair);
       else
-        launch_trial(g, pass, c->zc, c->tgt, c->Q, c->found, c->tr_part, nblk, s);
+        launch_trial(g, pass, c->zc, c->tgt, c->Q, c->found + 4 * (pass & 1), c->tr_part, nblk, s);
     }
-    launch_trial_reduce(g, pass, c->tr_part, nred, c->found, c->tr_sums, s);
-    rc = allreduce_f64(c, c->tr_sums, 4 * kTrialSlots, s);
-    if (rc) return rc;
     sa.pass = pass;
+    sa.found_in = c->found + 4 * (pass & 1);
+    sa.found_out = c->found + 4 * ((pass + 1) & 1);
+    if (fused_reduce) {   // k_select reduces the partials itself (no all-reduce in between)
+      sa.part = c->tr_part;
+      sa.nred = nred;
+    } else {
+      launch_trial_reduce(g, pass, c->tr_part, nred, sa.found_in, c->tr_sums, s);
+      rc = allreduce_f64(c, c->tr_sums, 4 * kTrialSlots, s);
+      if (rc) return rc;
+      sa.part = nullptr;
+    }
     launch_select(g, c->hp, sa, s);
   }
   return ADMM_OK;
@@ -496,7 +504,7 @@ int admm_create(const AdmmDims* dims, const AdmmParams* params, int device, Admm
       (rc = dalloc(&c->gslab, slab)) ||
       (rc = dalloc(&c->tr_part, (size_t)4 * kTrialSlots * c->nblk_trial)) ||
       (rc = dalloc(&c->tr_sums, (size_t)4 * kTrialSlots)) || (rc = dalloc(&c->tr_poly, (size_t)4 * kPolyN)) ||
-      (rc = dalloc(&c->found, 4)) || (rc = dalloc(&c->pick, 4)) ||
+      (rc = dalloc(&c->found, 8)) || (rc = dalloc(&c->pick, 4)) ||
       (rc = dalloc(&c->U, (size_t)g.B * g.O)) || (rc = dalloc(&c->wy_slab, (size_t)c->wy_nsplit * g.H * g.O)) ||
       (rc = dalloc(&c->Gy, (size_t)g.H * g.O)) || (rc = dalloc(&c->ht_part, (size_t)c->ht_nblk * kHTSums)) ||
       (rc = dalloc(&c->ht_sums, kHTSums)) || (rc = dalloc(&c->stats, 1)) || (rc = dalloc(&c->lamh_nz, 1)) ||

@@ -1413,7 +1413,7 @@ __global__ __launch_bounds__(kThreads) void k_trial(Geom g, int pass, const floa
 // update to the cached pre-activations on the fly, z = zc + x_row . dWx[:, j].
 
 // W <- (0.5 rho T theta* W - G) / (beta + 0.5 rho theta* T), theta* = 2^k / 2 (admm.py:338-343):
-// one definition for k_wupdate and the speculative x-stage z update (SpecX), which must
+// one definition for k_select and the speculative x-stage z update (SpecX), which must
 // reproduce its dWx bit for bit.
 struct WUpd {
   float c1, den;
@@ -1599,7 +1599,7 @@ __device__ __forceinline__ void trial_rows_body(const Geom& g, int q, int pass, 
   float gw[DP];
 #pragma unroll
   for (int d = 0; d < DP; ++d) gw[d] = (SIDE == 0 && d < g.D) ? Gx[((int64_t)q * g.D + d) * g.H + j] : 0.f;
-  // SPEC: this column of dWx for the predicted exponent, as k_wupdate will form it, parked in
+  // SPEC: this column of dWx for the predicted exponent, as k_select will form it, parked in
   // LDS as [DP/4][256] float4 (each thread reads back only its own column: no barrier) so the
   // kernel keeps its 4 waves per SIMD
   float* __restrict__ zxq = SPEC ? sp.zx + (int64_t)q * n + j : nullptr;
@@ -2024,28 +2024,63 @@ __global__ __launch_bounds__(kThreads) void k_trial_reduce(int pass, const doubl
   if (threadIdx.x == 0) sums[q * kSlots + k] = tot;
 }
 
-// First k with f(W + G/2^k) <= est_k (admm.py:331-336); then
-// W <- (0.5 rho T theta* W - G) / (beta + 0.5 rho theta* T), theta* = 2^k / 2 (admm.py:338-343).
-// lhs_k = 0.5 rho (per-candidate sum of this window + polynomial part at s = 2^-k);
-// rhs_k = est_k - f(W) = sum G (beta - W) + 0.5 T theta ||beta - W||^2 = (1 + T/2) ||G||^2 2^-k.
-// If every element was in the polynomial regime the decision extends over all k < kMaxK.
-// Selection of one pass (admm.py:331-338): per gate, the first exponent k of the window with
-// f(W + G/2^k) - f(W) <= (1 + T/2) ||G||^2 2^-k, in fp64 from the pass sums.
-__global__ __launch_bounds__(kThreads) void k_decide(Geom g, Hyper hp, SelectArgs a) {
-  __shared__ double red[4];
-  const int q = blockIdx.x;
-  if (a.found[q]) {   // decided in an earlier pass
-    if (threadIdx.x == 0) a.pick[q] = -1;
+// One trial pass's selection in one launch, grid (kSelBlocks, 4): every block of gate q
+//  1. reduces the pass's per-block partials (a.part, a.nred per slot; or reads the all-reduced
+//     a.sums when a.part is null, the multi-process path) in k_trial_reduce's order -- thread t
+//     sums partials t, t + 256, ..., then the fixed wave / cross-wave tree of block_sum -- so
+//     every block holds bit-identical sums;
+//  2. computes ||G||^2 in the same fixed order;
+//  3. takes the first k with f(W + G/2^k) - f(W) <= (1 + T/2) ||G||^2 2^-k (admm.py:331-338):
+//     lhs_k = 0.5 rho (per-candidate sum of this window + polynomial part at s = 2^-k), in fp64;
+//  4. updates its slice of W <- (0.5 rho T theta* W - G) / (beta + 0.5 rho theta* T),
+//     theta* = 2^k / 2 (admm.py:338-343), and dW.
+// Block 0 of the gate writes the stats and the flags.  The found flags are double-buffered by
+// pass parity (a.found_in read, a.found_out written): a block that starts after block 0 has
+// decided must still see the gate as undecided.
+constexpr int kSelBlocks = 16;
+
+__global__ __launch_bounds__(kThreads) void k_select(Geom g, Hyper hp, SelectArgs a) {
+  __shared__ double red[4][kSlots];
+  __shared__ double sums[kSlots];
+  __shared__ double gred[4];
+  __shared__ int pick_s;
+  const int q = blockIdx.y, mb = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  if (a.found_in[q]) {   // decided in an earlier pass
+    if (mb == 0 && tid == 0) {
+      a.found_out[q] = 1;
+      a.pick[q] = -1;
+    }
     return;
   }
+  // 1. the pass sums of this gate
+  if (a.part) {
+    double acc[kSlots];
+#pragma unroll
+    for (int k = 0; k < kSlots; ++k) acc[k] = 0.0;
+    const double* p = a.part + (int64_t)q * kSlots * a.nred;
+    for (int i = tid; i < a.nred; i += kThreads) {
+#pragma unroll
+      for (int k = 0; k < kSlots; ++k) acc[k] += p[(int64_t)k * a.nred + i];
+    }
+#pragma unroll
+    for (int k = 0; k < kSlots; ++k) {
+      const double v = wave_sum(acc[k]);
+      if (lane == 0) red[w][k] = v;
+    }
+    __syncthreads();
+    if (tid < kSlots) sums[tid] = (red[0][tid] + red[1][tid]) + (red[2][tid] + red[3][tid]);
+  } else if (tid < kSlots) {
+    sums[tid] = a.sums[q * kSlots + tid];
+  }
+  // 2. ||G||^2 (k_decide's order: float4 loads 8 at a time)
   const int Kd = a.side == 0 ? g.D : g.H;
   const int64_t nW = (int64_t)Kd * g.H;
   const float* Gq = a.G + (int64_t)q * nW;
   double gs = 0.0;
-  if ((nW & 3) == 0) {   // one block per gate: loads issued 8 float4 at a time, same summation order
+  if ((nW & 3) == 0) {
     const float4* G4 = reinterpret_cast<const float4*>(Gq);
     const int64_t n4 = nW / 4;
-    int64_t i = threadIdx.x;
+    int64_t i = tid;
     for (; i + 7 * kThreads < n4; i += 8 * kThreads) {
       float4 v[8];
 #pragma unroll
@@ -2059,14 +2094,18 @@ __global__ __launch_bounds__(kThreads) void k_decide(Geom g, Hyper hp, SelectArg
       gs += ((double)v.x * v.x + (double)v.y * v.y) + ((double)v.z * v.z + (double)v.w * v.w);
     }
   } else {
-    for (int64_t i = threadIdx.x; i < nW; i += kThreads) gs += (double)Gq[i] * (double)Gq[i];
+    for (int64_t i = tid; i < nW; i += kThreads) gs += (double)Gq[i] * (double)Gq[i];
   }
-  const double gsq = block_sum(gs, red);
+  const double gsq = block_sum(gs, gred);   // (its barriers also publish sums[])
   const float rho = hp.rho[q];
-  if (threadIdx.x == 0) {
-    const double* sm = a.sums + q * kSlots;
-    if (a.pass == 0)
-      for (int n = 0; n < kPolyN; ++n) a.poly[q * kPolyN + n] = sm[kSlotPoly + n];
+  // 3. the decision
+  if (tid == 0) {
+    const double* sm = sums;
+    double* pq = a.poly + q * kPolyN;
+    double pl[kPolyN];
+    for (int n = 0; n < kPolyN; ++n) pl[n] = a.pass == 0 ? sm[kSlotPoly + n] : pq[n];
+    if (a.pass == 0 && mb == 0)
+      for (int n = 0; n < kPolyN; ++n) pq[n] = pl[n];
     const bool poly_only = sm[kSlotNne] == 0.0;
     const int k_lo = poly_only ? 0 : a.pass * kTrialJ;
     const int k_hi = poly_only ? kMaxK : k_lo + kTrialJ;
@@ -2074,46 +2113,41 @@ __global__ __launch_bounds__(kThreads) void k_decide(Geom g, Hyper hp, SelectArg
     for (int kk = k_lo; kk < k_hi; ++kk) {
       const double sk = ldexp(1.0, -kk);
       double poly = 0.0;
-      for (int n = kPolyN - 1; n >= 0; --n) poly = (poly + a.poly[q * kPolyN + n]) * sk;
+      for (int n = kPolyN - 1; n >= 0; --n) poly = (poly + pl[n]) * sk;
       const double cand = poly_only ? 0.0 : sm[kk - k_lo];
       const double lhs = 0.5 * (double)rho * (cand + poly);
       const double rhs = (1.0 + 0.5 * g.T) * gsq * sk;
-      if (!isfinite(lhs)) atomicAdd(&a.stats->nonfinite, 1);
+      if (!isfinite(lhs) && mb == 0) atomicAdd(&a.stats->nonfinite, 1);
       if (lhs > rhs) continue;
       pick = kk;
       break;
     }
     if (pick < 0 && (poly_only || a.pass == a.last_pass)) {
       pick = k_hi;
-      atomicAdd(&a.stats->unresolved, 1);
+      if (mb == 0) atomicAdd(&a.stats->unresolved, 1);
     }
-    if (pick >= 0) {
-      const int slot = 2 * q + a.side;
-      a.stats->k[slot] = pick;
-      a.stats->f_w[slot] = 0.5 * (double)rho * sm[kSlotFw];
-      a.stats->grad_sq[slot] = gsq;
-      a.stats->direct_frac[slot] = sm[kSlotNne] / ((double)g.Bg * g.T * g.H);
-      a.stats->passes[a.side] = a.pass + 1;
-      a.found[q] = 1;
+    if (mb == 0) {
+      if (pick >= 0) {
+        const int slot = 2 * q + a.side;
+        a.stats->k[slot] = pick;
+        a.stats->f_w[slot] = 0.5 * (double)rho * sm[kSlotFw];
+        a.stats->grad_sq[slot] = gsq;
+        a.stats->direct_frac[slot] = sm[kSlotNne] / ((double)g.Bg * g.T * g.H);
+        a.stats->passes[a.side] = a.pass + 1;
+      }
+      a.found_out[q] = pick >= 0 ? 1 : 0;
+      a.pick[q] = pick;
     }
-    a.pick[q] = pick;
+    pick_s = pick;
   }
-}
-
-// W <- (0.5 rho T theta* W - G) / (beta + 0.5 rho theta* T), theta* = 2^k / 2 (admm.py:338-343),
-// for the gates decided in this pass; grid (blocks, 4).
-__global__ __launch_bounds__(kThreads) void k_wupdate(Geom g, Hyper hp, SelectArgs a) {
-  const int q = blockIdx.y;
-  const int pick = a.pick[q];
+  __syncthreads();
+  const int pick = pick_s;
   if (pick < 0) return;
-  const int Kd = a.side == 0 ? g.D : g.H;
-  const int64_t nW = (int64_t)Kd * g.H;
-  const float* Gq = a.G + (int64_t)q * nW;
-  const float rho = hp.rho[q];
+  // 4. this block's slice of the weight update
   const float beta = a.side == 0 ? hp.beta_x[q] : hp.beta_h[q];
   const WUpd u = WUpd::make(rho, beta, g.T, pick);
   float* W = a.W[q];
-  for (int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x; i < nW; i += (int64_t)gridDim.x * kThreads) {
+  for (int64_t i = (int64_t)mb * kThreads + tid; i < nW; i += (int64_t)gridDim.x * kThreads) {
     const float w0 = W[i];
     const float w1 = u.apply(w0, Gq[i]);
     W[i] = w1;
@@ -2697,10 +2731,7 @@ void launch_trial_fast(const Geom& g, int side, int pass, const float* zc, const
 }
 
 void launch_select(const Geom& g, const Hyper& hp, const SelectArgs& a, hipStream_t s) {
-  k_decide<<<4, kThreads, 0, s>>>(g, hp, a);
-  const int64_t nW = (int64_t)(a.side == 0 ? g.D : g.H) * g.H;
-  dim3 grid(std::max(1, std::min(cdiv64(nW, kThreads * 4), 256)), 4);
-  k_wupdate<<<grid, kThreads, 0, s>>>(g, hp, a);
+  k_select<<<dim3(kSelBlocks, 4), kThreads, 0, s>>>(g, hp, a);
 }
 
 int wy_splits(const Geom& g) {

@@ -161,7 +161,7 @@ void launch_resid_gx(const Geom& g, const Hyper& hp, const float* x, const Plane
 // trial pass without a materialised Q (side 0: q = x.G_x) or z (side 1: z = zc + x.dWx)
 // Speculative Gauss-Seidel z update of the x stage (H % 256 == 0): pass 0 of the x-side trials
 // also writes zx = zc + x dWx(kpred) for the exponent the gate took in the previous step
-// (kpred, copied from the stats by k_reduce_g), with dWx formed exactly as k_wupdate forms it;
+// (kpred, copied from the stats by k_reduce_g), with dWx formed exactly as k_select forms it;
 // k_apply_fix recomputes zx only for the gates whose decided exponent differs.
 struct SpecX {
   const int* kpred;         // [4] predicted x-side exponent per gate
@@ -214,13 +214,16 @@ void launch_qgemm3_img(const Geom& g, const float* Sh, const float* gimg, float*
 struct SelectArgs {
   int side;                 // 0 x, 1 h
   int pass, last_pass;
-  const double* sums;       // [4][kTrialSlots] of this pass
+  const double* part;       // [4][kTrialSlots][nred] per-block partials of this pass (single process), or
+  int nred;
+  const double* sums;       // [4][kTrialSlots] all-reduced sums of this pass (part == nullptr)
   double* poly;             // [4][kPolyN] polynomial coefficients kept from pass 0
   const float* G;           // [4][K][H]
   float* W[4];              // weights being updated (in place)
   float* dW;                // [4][K][H] W_new - W_old (side 0), nullable
-  int* found;
-  int* pick;                // [4] exponent chosen in this pass, -1 if none (k_decide -> k_wupdate)
+  const int* found_in;      // [4] decided before this pass (found + 4 (pass & 1))
+  int* found_out;           // [4] decided after it (found + 4 ((pass + 1) & 1))
+  int* pick;                // [4] exponent chosen in this pass, -1 if none
   DevStats* stats;
 };
 void launch_select(const Geom& g, const Hyper& hp, const SelectArgs& a, hipStream_t s);

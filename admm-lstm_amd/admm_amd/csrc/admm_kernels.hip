@@ -2207,7 +2207,15 @@ __global__ __launch_bounds__(kThreads) void k_wy_reduce(int64_t nHO, const float
   const int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x;
   if (i >= nHO) return;
   double s = 0.0;
-  for (int sp = 0; sp < nsplit; ++sp) s += (double)slab[(int64_t)sp * nHO + i];
+  int sp = 0;
+  for (; sp + 8 <= nsplit; sp += 8) {   // loads issued 8 at a time, the same summation order
+    float v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = slab[(int64_t)(sp + u) * nHO + i];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) s += (double)v[u];
+  }
+  for (; sp < nsplit; ++sp) s += (double)slab[(int64_t)sp * nHO + i];
   Gy[i] = (float)s;
 }
 
@@ -2329,13 +2337,27 @@ __global__ __launch_bounds__(kThreads) void k_ht_partial(Geom g, Hyper hp, Plane
   (void)red;
 }
 
+// all kHTSums sums in one pass over the partials (per sum: thread t adds partials t, t + 256, ...,
+// then block_sum's fixed tree -- the order of a per-sum loop, one barrier instead of 2 kHTSums)
 __global__ __launch_bounds__(kThreads) void k_ht_reduce(const double* part, int nblk, double* sums) {
-  __shared__ double red[4];
+  __shared__ double red[4][kHTSums];
+  double s[kHTSums];
+#pragma unroll
+  for (int i = 0; i < kHTSums; ++i) s[i] = 0.0;
+  for (int b = threadIdx.x; b < nblk; b += kThreads) {
+#pragma unroll
+    for (int i = 0; i < kHTSums; ++i) s[i] += part[(int64_t)b * kHTSums + i];
+  }
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
   for (int i = 0; i < kHTSums; ++i) {
-    double s = 0.0;
-    for (int b = threadIdx.x; b < nblk; b += kThreads) s += part[(int64_t)b * kHTSums + i];
-    const double tot = block_sum(s, red);
-    if (threadIdx.x == 0) sums[i] = tot;
+    const double v = wave_sum(s[i]);
+    if (lane == 0) red[w][i] = v;
+  }
+  __syncthreads();
+  if (threadIdx.x < kHTSums) {
+    const int i = threadIdx.x;
+    sums[i] = (red[0][i] + red[1][i]) + (red[2][i] + red[3][i]);
   }
 }
 
@@ -2734,9 +2756,9 @@ void launch_select(const Geom& g, const Hyper& hp, const SelectArgs& a, hipStrea
   k_select<<<dim3(kSelBlocks, 4), kThreads, 0, s>>>(g, hp, a);
 }
 
-int wy_splits(const Geom& g) {
-  int ns = cdiv64(g.B, 256);
-  return ns > 256 ? 256 : (ns < 1 ? 1 : ns);
+int wy_splits(const Geom& g) {   // 64 rows per split: the strided h_T loads are latency-bound
+  int ns = cdiv64(g.B, 64);
+  return ns > 512 ? 512 : (ns < 1 ? 1 : ns);
 }
 
 void launch_wy_grad(const Geom& g, const Hyper& hp, const float* Sh, const float* a, const float* Ly,
@@ -2759,9 +2781,9 @@ void launch_wy_apply(const Geom& g, const Hyper& hp, const float* Gy, float* wy,
   k_wy_apply<<<cdiv64(nHO, kThreads), kThreads, 0, s>>>(nHO, hp, Gy, wy);
 }
 
-int ht_blocks(const Geom& g) {
+int ht_blocks(const Geom& g) {   // one row per wave up to B = 8192 (each row is a latency chain)
   int nb = cdiv64(g.B, 4);
-  return nb > 1024 ? 1024 : nb;
+  return nb > 2048 ? 2048 : nb;
 }
 
 void launch_ht_partial(const Geom& g, const Hyper& hp, const Planes6& S, const Planes6& L, const float* a,

@@ -215,10 +215,6 @@ def main():
     x = x_all[rank * per:(rank + 1) * per].contiguous().to(dev)
     y = y_all[rank * per:(rank + 1) * per].contiguous().to(dev)
     del x_all, y_all
-    torch.manual_seed(0)
-    model = LSTM(D, H, 1).to(dev)
-    opt = mod.ADMMBasedOptimizer(model, (x, y), example_parameter_dictionary['GoogleStock'], verbose=False,
-                                 distributed=world > 1)
 
     def barrier():
         torch.cuda.synchronize(dev)
@@ -226,18 +222,36 @@ def main():
             dist.barrier()
         torch.cuda.synchronize(dev)
 
-    for _ in range(args.warmup):
+    def fresh():
+        torch.manual_seed(0)
+        m = LSTM(D, H, 1).to(dev)
+        o = mod.ADMMBasedOptimizer(m, (x, y), example_parameter_dictionary['GoogleStock'], verbose=False,
+                                   distributed=world > 1)
+        for _ in range(args.warmup):
+            o.step()
+        barrier()
+        return m, o
+
+    # kernel classes: hipEvent pairs around each class on the step's stream over the steps the
+    # timed run below takes (same seed and data: the same trajectory); the event records cost
+    # about 0.2 ms per step, so this run is not the timed one
+    classes = [c for c in args.profile_classes.split(',') if c]
+    model, opt = fresh()
+    opt.profile(classes)
+    for _ in range(args.steps):
         opt.step()
     barrier()
-    classes = [c for c in args.profile_classes.split(',') if c]
-    opt.profile(classes)
+    opt.profile(())
+    prof = opt.profile_read()
+    del opt, model
+    torch.cuda.empty_cache()
+    # timed region: plain steps, no events between the launches
+    model, opt = fresh()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         opt.step()
     barrier()
     elapsed = time.perf_counter() - t0
-    opt.profile(())
-    prof = opt.profile_read()
     if dist is not None:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)

@@ -73,12 +73,28 @@ __device__ __forceinline__ float expm1_acc(float x) {
 // (p_i q_j exact in the MFMA's f32 accumulation) reproduce an f32 product to ~2^-26 relative,
 // at the bf16 matrix rate: 6 x v_mfma_f32_32x32x16_bf16 (192 cycles) per 16-deep step against
 // 8 x v_mfma_f32_32x32x2_f32 (512 cycles, and those hold the SIMD's VALU issue).
+// The f32 value of each rounded piece is read back from the packed dword of its pair (low half
+// << 16, high half & 0xffff0000): one v_cvt_pk_bf16_f32 per pair and piece, where converting the
+// bf16 vector back costs a second, single-lane v_cvt_pk per element.  Same pieces, bit for bit.
+template <class V, class B>
+__device__ __forceinline__ V bf16_widen(B p) {
+  constexpr int N = sizeof(V) / 4;
+  typedef unsigned U __attribute__((ext_vector_type(N / 2)));
+  const U w = __builtin_bit_cast(U, p);
+  V f;
+#pragma unroll
+  for (int i = 0; i < N / 2; ++i) {
+    f[2 * i] = __builtin_bit_cast(float, w[i] << 16);
+    f[2 * i + 1] = __builtin_bit_cast(float, w[i] & 0xffff0000u);
+  }
+  return f;
+}
 template <class V, class B>
 __device__ __forceinline__ void split3(V a, B& p0, B& p1, B& p2) {
   p0 = __builtin_convertvector(a, B);
-  const V r1 = a - __builtin_convertvector(p0, V);
+  const V r1 = a - bf16_widen<V>(p0);
   p1 = __builtin_convertvector(r1, B);
-  const V r2 = r1 - __builtin_convertvector(p1, V);
+  const V r2 = r1 - bf16_widen<V>(p1);
   p2 = __builtin_convertvector(r2, B);
 }
 __device__ __forceinline__ void split3(float a, __bf16& p0, __bf16& p1, __bf16& p2) {

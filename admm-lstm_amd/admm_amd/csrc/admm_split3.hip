@@ -330,15 +330,9 @@ __device__ __forceinline__ void atr3w_body(const Geom& g, int q, int sp, int nsp
   using P = A3<256>;
   const int H = g.H;
   const int64_t BT = g.BT();
-#ifndef A3W_INTERLEAVE
-#define A3W_INTERLEAVE 0
-#endif
-  // A3W_INTERLEAVE: the workgroups of a gate take 16-row steps round robin (step i of split sp is
-  // rows 16 (sp + i nsplit) ..), so at any time they read adjacent rows, not rows 4 MB apart
   const int64_t per = ((BT + nsplit - 1) / nsplit + A3_KS - 1) / A3_KS * A3_KS;
-  const int64_t r0 = A3W_INTERLEAVE ? (int64_t)sp * A3_KS : sp * per;
-  const int64_t r1 = A3W_INTERLEAVE ? BT : (r0 + per < BT ? r0 + per : BT);
-  const int64_t ks = A3W_INTERLEAVE ? (int64_t)nsplit * A3_KS : A3_KS;   // rows from one step to the next
+  const int64_t r0 = sp * per, r1 = r0 + per < BT ? r0 + per : BT;
+  constexpr int64_t ks = A3_KS;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int rg = __builtin_amdgcn_readfirstlane(wave);   // rows 2 rg, 2 rg + 1 of each step
   const __amdgpu_buffer_rsrc_t rA = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(Sh), 0,

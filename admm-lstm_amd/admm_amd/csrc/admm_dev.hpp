@@ -16,6 +16,7 @@ namespace admm {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 
@@ -213,6 +214,15 @@ __device__ __forceinline__ float buf_ld(__amdgpu_buffer_rsrc_t r, uint32_t off) 
 template <int AUX = 2>
 __device__ __forceinline__ f32x4 buf_ld4(__amdgpu_buffer_rsrc_t r, uint32_t off) {
   return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, AUX));
+}
+template <int AUX = 2>
+__device__ __forceinline__ f32x2 buf_ld2(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+  return __builtin_bit_cast(f32x2, __builtin_amdgcn_raw_buffer_load_b64(r, (int)off, 0, AUX));
+}
+template <int AUX = 2>
+__device__ __forceinline__ void buf_st2(__amdgpu_buffer_rsrc_t r, uint32_t off, f32x2 v) {
+  __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(__attribute__((ext_vector_type(2))) unsigned int, v), r,
+                                        (int)off, 0, AUX);
 }
 template <int AUX = 2>
 __device__ __forceinline__ void buf_st4(__amdgpu_buffer_rsrc_t r, uint32_t off, f32x4 v) {

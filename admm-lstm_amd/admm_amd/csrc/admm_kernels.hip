@@ -1721,9 +1721,17 @@ __device__ __forceinline__ void trial_mx_body(const Geom& g, int q, int pass, co
   const int64_t BT = g.BT(), n = BT * g.H;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int col0 = (blockIdx.z * 4 + wave) * 32 + 2 * (lane & 15);   // this lane's column pair
-  const float* __restrict__ zq = zc + (int64_t)q * n + col0;
-  const float* __restrict__ tq = tgt + (int64_t)q * n + col0;
-  float* __restrict__ zxq = SPEC ? sp.zx + (int64_t)q * n + col0 : nullptr;
+  // 32-bit buffer offsets into one gate plane (trial_mx_ok: a plane is < 2 GB); rows past BT
+  // are past the descriptor's range, so they load 0 and their stores are dropped (and the
+  // trial arithmetic masks them with ok below)
+  const __amdgpu_buffer_rsrc_t rZ = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(zc + (int64_t)q * n), 0, (int)(n * 4), kBufWord3);
+  const __amdgpu_buffer_rsrc_t rT = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(tgt + (int64_t)q * n), 0, (int)(n * 4), kBufWord3);
+  const __amdgpu_buffer_rsrc_t rX = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(x), 0, (int)(BT * g.D * 4), kBufWord3);
+  const __amdgpu_buffer_rsrc_t rZX = SPEC ? __builtin_amdgcn_make_buffer_rsrc(sp.zx + (int64_t)q * n, 0, (int)(n * 4), kBufWord3)
+                                          : rZ;
+  const uint32_t rowb = (uint32_t)g.H * 4;   // bytes per row of a plane
+  // this lane's byte offset within a tile: row 4 (lane / 16), columns col0, col0 + 1
+  const uint32_t lofs = (uint32_t)(4 * (lane >> 4)) * rowb + (uint32_t)col0 * 4;
   // B operands: row 4 s + lane/16 of G_x (and dWx) at column col0 + h (product h)
   float gb[2][4], db[2][4];
   const WUpd u = SPEC ? WUpd::make(sp.hp.rho[q], sp.hp.beta_x[q], g.T, sp.kpred[q]) : WUpd{};
@@ -1747,19 +1755,19 @@ __device__ __forceinline__ void trial_mx_body(const Geom& g, int q, int pass, co
   // BT clamped: branch-free, masked by ok below)
   struct In { float xa[4]; f32x2 zv[4], tv[4]; };
   auto load = [&](int64_t tile, In& v) {
-    const int64_t row0 = tile * 16;
+    const uint32_t row0 = (uint32_t)tile * 16;
     // A operand: x[row0 + lane % 16][4 s + lane / 16]
-    const int64_t xr = min(row0 + (lane & 15), BT - 1);
+    const uint32_t xo = ((row0 + (lane & 15)) * g.D + (lane >> 4)) * 4;
 #pragma unroll
     for (int s4 = 0; s4 < 4; ++s4) {
       const int d = 4 * s4 + (lane >> 4);
-      v.xa[s4] = d < g.D ? x[xr * g.D + d] : 0.f;
+      v.xa[s4] = d < g.D ? buf_ld<0>(rX, xo + 16 * s4) : 0.f;
     }
+    const uint32_t o = row0 * rowb + lofs;
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const int64_t row = min(row0 + 4 * (lane >> 4) + r, BT - 1);
-      v.zv[r] = __builtin_nontemporal_load(reinterpret_cast<const f32x2*>(zq + row * g.H));
-      v.tv[r] = __builtin_nontemporal_load(reinterpret_cast<const f32x2*>(tq + row * g.H));
+      v.zv[r] = buf_ld2(rZ, o + r * rowb);
+      v.tv[r] = buf_ld2(rT, o + r * rowb);
     }
   };
   In cur, nxt;
@@ -1780,12 +1788,9 @@ __device__ __forceinline__ void trial_mx_body(const Geom& g, int q, int pass, co
       for (int s4 = 0; s4 < 4; ++s4)
 #pragma unroll
         for (int h = 0; h < 2; ++h) da[h] = __builtin_amdgcn_mfma_f32_16x16x4f32(xa[s4], db[h][s4], da[h], 0, 0, 0);
+      const uint32_t o = (uint32_t)row0 * rowb + lofs;
 #pragma unroll
-      for (int v = 0; v < 4; ++v) {
-        const int64_t row = row0 + 4 * (lane >> 4) + v;
-        if (row < BT)
-          __builtin_nontemporal_store(zv[v] + f32x2{da[0][v], da[1][v]}, reinterpret_cast<f32x2*>(zxq + row * g.H));
-      }
+      for (int v = 0; v < 4; ++v) buf_st2(rZX, o + v * rowb, zv[v] + f32x2{da[0][v], da[1][v]});
     }
 #pragma unroll
     for (int v = 0; v < 4; ++v) {   // the two columns of row 4 (lane / 16) + v
@@ -1799,8 +1804,11 @@ __device__ __forceinline__ void trial_mx_body(const Geom& g, int q, int pass, co
   dq_run(dq, acc, true);
 }
 
+#ifndef TMX_MINB
+#define TMX_MINB 3
+#endif
 template <bool SPEC>
-__global__ __launch_bounds__(kThreads, 3) void k_trial_mx(Geom g, int pass, const float* __restrict__ zc,
+__global__ __launch_bounds__(kThreads, TMX_MINB) void k_trial_mx(Geom g, int pass, const float* __restrict__ zc,
                                                        const float* __restrict__ tgt, const float* __restrict__ x,
                                                        const float* __restrict__ Gx, const int* __restrict__ found,
                                                        double* __restrict__ part, int nblk, SpecX sp) {
@@ -2703,7 +2711,8 @@ bool trial_mx_ok(const Geom& g) {   // ADMM_TRIAL_MX=0: the x side on k_trial_ro
     const char* e = std::getenv("ADMM_TRIAL_MX");
     g_trial_mx = e ? std::atoi(e) != 0 : 1;
   }
-  return g_trial_mx && g.H % 256 == 0 && g.D <= 16;
+  // 32-bit buffer offsets within one gate plane
+  return g_trial_mx && g.H % 256 == 0 && g.D <= 16 && g.BT() * g.H * 4 < (int64_t)INT32_MAX;
 }
 
 void launch_trial_fast(const Geom& g, int side, int pass, const float* zc, const float* tgt, const float* Q,

@@ -123,7 +123,7 @@ struct AdmmCtx {
   // rounding of W + G/theta (DESIGN.md "trial direction precision"); G itself stays split3.
   int q_pieces = 2;
   bool atr3w = true;
-  // Q in the row-pair layout (k_qgemm3 -> k_trial_rows<1>; ADMM_QPAIR=0: row-major)
+  // Q in the row-quad layout (k_qgemm3 -> k_trial_rows<1>; ADMM_QPAIR=0: row-major)
   bool qpair = true;       // k_atr3w (two waves per SIMD) for the h-side gradient; ADMM_ATR3W=0: k_atr3
   float* gimg = nullptr;   // split image of G_h for k_qgemm3
   hipStream_t sx[kMaxSweepStreams - 1] = {};

@@ -1583,8 +1583,8 @@ __global__ __launch_bounds__(kThreads, TF_MINB) void k_trial_fast(Geom g, int pa
 // are wave-uniform (scalar loads, SGPR operands) and the thread's column of G_x stays in 16
 // VGPRs for the whole pass: q = x_row . G_x costs 16 FMAs and no LDS.  The two rows are the two
 // halves of trial_pair's packed arithmetic; the next pair's operands are loaded while this one
-// is evaluated.  Side 1 reads q from Q instead (QP: Q in k_qgemm3's row-pair layout
-// [row / 2][j][row % 2], one float2 per pair).
+// is evaluated.  Side 1 reads q from Q instead and walks row quads (QP: Q in k_qgemm3's
+// row-quad layout [row / 4][j][row % 4], one float4 per quad).
 template <bool TANH, int SIDE, int DP, bool XV, bool SPEC, bool QP = false>
 __device__ __forceinline__ void trial_rows_body(const Geom& g, int q, int pass, const float* __restrict__ zc,
                                                 const float* __restrict__ tgt, const float* __restrict__ Q,
@@ -1595,7 +1595,7 @@ __device__ __forceinline__ void trial_rows_body(const Geom& g, int q, int pass, 
   const int j = blockIdx.z * 256 + threadIdx.x;
   const float* __restrict__ zq = zc + (int64_t)q * n + j;
   const float* __restrict__ tq = tgt + (int64_t)q * n + j;
-  const float* __restrict__ Qq = Q ? Q + (int64_t)q * n + (QP ? 2 * j : j) : nullptr;
+  const float* __restrict__ Qq = Q ? Q + (int64_t)q * n + (QP ? 4 * j : j) : nullptr;
   float gw[DP];
 #pragma unroll
   for (int d = 0; d < DP; ++d) gw[d] = (SIDE == 0 && d < g.D) ? Gx[((int64_t)q * g.D + d) * g.H + j] : 0.f;
@@ -1617,6 +1617,55 @@ __device__ __forceinline__ void trial_rows_body(const Geom& g, int q, int pass, 
       dwl[d4 * 256 + threadIdx.x] = make_float4(v[0], v[1], v[2], v[3]);
     }
   }
+  f32x2 acc2[kPair];
+#pragma unroll
+  for (int k = 0; k < kPair; ++k) acc2[k] = f32x2{0.f, 0.f};
+  if constexpr (SIDE == 1) {
+    // h side: row quads (two row pairs per iteration), so that one Q load in the row-quad
+    // layout (QP) covers the iteration; the row-major path walks the same quads (same sums)
+    struct In4 { f32x2 z[2], t[2], q[2]; };
+    auto load4 = [&](int64_t ra, In4& v) {   // rows ra .. ra + 3 (clamped); ra % 4 == 0
+      int64_t r[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) r[i] = __builtin_amdgcn_readfirstlane((int)(ra + i < BT ? ra + i : BT - 1));
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        v.z[h] = f32x2{__builtin_nontemporal_load(zq + r[2 * h] * g.H), __builtin_nontemporal_load(zq + r[2 * h + 1] * g.H)};
+        v.t[h] = f32x2{__builtin_nontemporal_load(tq + r[2 * h] * g.H), __builtin_nontemporal_load(tq + r[2 * h + 1] * g.H)};
+      }
+      if constexpr (QP) {   // BT % 4 == 0: one quad
+        const int64_t pr = __builtin_amdgcn_readfirstlane((int)((ra < BT ? ra : BT - 4) >> 2));
+        const f32x4 qq = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(Qq + pr * 4 * g.H));
+        v.q[0] = f32x2{qq[0], qq[1]};
+        v.q[1] = f32x2{qq[2], qq[3]};
+      } else {
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+          v.q[h] = f32x2{__builtin_nontemporal_load(Qq + r[2 * h] * g.H), __builtin_nontemporal_load(Qq + r[2 * h + 1] * g.H)};
+      }
+    };
+    const int64_t stride = 4 * (int64_t)nblk;
+    int64_t base = 4 * (int64_t)blk;
+    In4 cur, nxt;
+    load4(base, cur);
+    for (; base < BT; base += stride) {
+      load4(base + stride, nxt);
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        // rows past the end (BT % 4 != 0): a pair entirely past it is skipped (uniform), the
+        // second row of a pair is masked through its q and d0 (ok covers the pair)
+        if (h == 1 && base + 2 >= BT) break;
+        const bool ok1 = base + 2 * h + 1 < BT;
+        trial_pair<TANH>(true, cur.z[h], ok1 ? cur.t[h] : f32x2{cur.t[h].x, 0.f},
+                         ok1 ? cur.q[h] : f32x2{cur.q[h].x, 0.f}, pass, acc, acc2, dq, ok1);
+        dq_run(dq, acc, false);
+      }
+      cur = nxt;
+    }
+    trial_pair_fold(acc, acc2);
+    dq_run(dq, acc, true);
+    return;
+  }
   struct In { f32x2 z, t, q; float xa[DP], xb[DP]; };
   auto load = [&](int64_t ra, In& v) {   // rows ra, ra + 1 (clamped)
     const int64_t r0 = __builtin_amdgcn_readfirstlane((int)(ra < BT ? ra : BT - 1));
@@ -1626,16 +1675,10 @@ __device__ __forceinline__ void trial_rows_body(const Geom& g, int q, int pass, 
     if (SIDE == 0) {
       load_xrow<DP, XV>(x, r0, g.D, v.xa);
       load_xrow<DP, XV>(x, r1, g.D, v.xb);
-    } else if constexpr (QP) {   // ra is even and BT is even: rows ra, ra + 1 are one pair
-      const int64_t pr = __builtin_amdgcn_readfirstlane((int)((ra < BT ? ra : BT - 2) >> 1));
-      v.q = __builtin_nontemporal_load(reinterpret_cast<const f32x2*>(Qq + pr * 2 * g.H));
     } else {
       v.q = f32x2{__builtin_nontemporal_load(Qq + r0 * g.H), __builtin_nontemporal_load(Qq + r1 * g.H)};
     }
   };
-  f32x2 acc2[kPair];
-#pragma unroll
-  for (int k = 0; k < kPair; ++k) acc2[k] = f32x2{0.f, 0.f};
   const int64_t stride = 2 * (int64_t)nblk;
   int64_t base = 2 * (int64_t)blk;
   In cur, nxt;

@@ -201,7 +201,7 @@ void launch_atr3(const Geom& g, const float* Sh, const float* zc, const float* t
                  hipStream_t s, bool two_waves = true);
 // pieces = 3: f32-accurate split3 products; 2: two-way splits, three products (~2^-16 relative),
 // enough for the trial direction ("trial direction precision")
-// qpair (and qpair_ok: BT even): Q in the row-pair layout [q][row / 2][j][row % 2] that
+// qpair (and qpair_ok: BT % 4 == 0): Q in the row-quad layout [q][row / 4][j][row % 4] that
 // launch_trial_fast(..., qpair = true) reads (the h-side trial pass, H % 256 == 0)
 bool qpair_ok(const Geom& g);
 void launch_qgemm3(const Geom& g, const float* Sh, const float* G, float* gimg, float* Q, hipStream_t s,

@@ -49,10 +49,11 @@ __global__ __launch_bounds__(kThreads) void k_split_g(int H, const float* __rest
 // One 128 x 256 tile of one gate per workgroup (qgemm3_tile).  found != nullptr: gates whose
 // line search has already decided are skipped (the later trial passes, when pass 0 ran fused
 // in k_qtrial3 and Q was never formed).
-// QP: Q is written in the row-pair layout Q[q][row / 2][j][row % 2] (BT even): registers r and
-// r + 1 of a 32x32 accumulator hold rows 2i, 2i + 1 of one column, so each lane stores 8 B and a
-// wave-instruction two contiguous 256-B runs -- half the store instructions of the row-major
-// layout (the epilogue is store-issue bound); the h-side trial reads a row pair as one float2.
+// QP: Q is written in the row-quad layout Q[q][row / 4][j][row % 4] (BT % 4 == 0): registers
+// 4i .. 4i + 3 of a 32x32 accumulator hold four consecutive rows of one column, so each lane
+// stores 16 B and a wave-instruction two contiguous 512-B runs -- a quarter of the store
+// instructions of the row-major layout (the epilogue is store-issue bound); the h-side trial
+// reads a row pair (rows 2i, 2i + 1: one half of a quad) as one float2.
 template <int NP, bool QP>
 __global__ __launch_bounds__(kThreads) void k_qgemm3(Geom g, const float* __restrict__ Sh,
                                                       const bf16x8* __restrict__ gi, float* __restrict__ Q,
@@ -70,17 +71,17 @@ __global__ __launch_bounds__(kThreads) void k_qgemm3(Geom g, const float* __rest
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, wr = wave >> 1, wc = wave & 1, c32 = lane & 31;
   float* Qq = Q + (int64_t)q * BT * H + Q3_BN * cb + wc * 128 + c32;
   if constexpr (QP) {
-    typedef float f32x2 __attribute__((ext_vector_type(2)));
-    f32x2* Qp = reinterpret_cast<f32x2*>(Q + (int64_t)q * BT * H) + Q3_BN * cb + wc * 128 + c32;
+    f32x4* Qp = reinterpret_cast<f32x4*>(Q + (int64_t)q * BT * H) + Q3_BN * cb + wc * 128 + c32;
 #pragma unroll
     for (int mi = 0; mi < 2; ++mi)
 #pragma unroll
-      for (int r = 0; r < 16; r += 2) {
-        const int64_t row = m0 + wr * 64 + mi * 32 + acc_row(r, lane);   // even
+      for (int r = 0; r < 16; r += 4) {
+        const int64_t row = m0 + wr * 64 + mi * 32 + acc_row(r, lane);   // a multiple of 4
         if (row >= BT) continue;
 #pragma unroll
         for (int ni = 0; ni < 4; ++ni)
-          __builtin_nontemporal_store(f32x2{acc[mi][ni][r], acc[mi][ni][r + 1]}, Qp + (row >> 1) * H + ni * 32);
+          __builtin_nontemporal_store(f32x4{acc[mi][ni][r], acc[mi][ni][r + 1], acc[mi][ni][r + 2], acc[mi][ni][r + 3]},
+                                      Qp + (row >> 2) * H + ni * 32);
       }
     return;
   }
@@ -480,7 +481,7 @@ void launch_split_g(const Geom& g, const float* G, float* gimg, hipStream_t s) {
   k_split_g<<<(total + kThreads - 1) / kThreads, kThreads, 0, s>>>(g.H, G, reinterpret_cast<bf16x8*>(gimg));
 }
 
-bool qpair_ok(const Geom& g) { return g.BT() % 2 == 0; }
+bool qpair_ok(const Geom& g) { return g.BT() % 4 == 0; }
 
 void launch_qgemm3_img(const Geom& g, const float* Sh, const float* gimg, float* Q, const int* found, hipStream_t s,
                        int pieces, bool qpair) {

@@ -80,8 +80,9 @@ __global__ __launch_bounds__(kThreads) void k_qgemm3(Geom g, const float* __rest
         if (row >= BT) continue;
 #pragma unroll
         for (int ni = 0; ni < 4; ++ni)
-          __builtin_nontemporal_store(f32x4{acc[mi][ni][r], acc[mi][ni][r + 1], acc[mi][ni][r + 2], acc[mi][ni][r + 3]},
-                                      Qp + (row >> 2) * H + ni * 32);
+          if (!(S3_ABL & 16) || acc[mi][ni][r] == 12345.f)
+            __builtin_nontemporal_store(f32x4{acc[mi][ni][r], acc[mi][ni][r + 1], acc[mi][ni][r + 2], acc[mi][ni][r + 3]},
+                                        Qp + (row >> 2) * H + ni * 32);
       }
     return;
   }

@@ -54,20 +54,20 @@ __global__ __launch_bounds__(kThreads) void k_split_g(int H, const float* __rest
 // stores 16 B and a wave-instruction two contiguous 512-B runs -- a quarter of the store
 // instructions of the row-major layout (the epilogue is store-issue bound); the h-side trial
 // reads a row pair (rows 2i, 2i + 1: one half of a quad) as one float2.
-template <int NP, bool QP>
-__global__ __launch_bounds__(kThreads) void k_qgemm3(Geom g, const float* __restrict__ Sh,
-                                                      const bf16x8* __restrict__ gi, float* __restrict__ Q,
-                                                      const int* __restrict__ found) {
-  __shared__ __attribute__((aligned(16))) char lds[kQ3Lds];
+template <int NP, bool QP, int BM>
+__global__ __launch_bounds__(2 * BM) void k_qgemm3(Geom g, const float* __restrict__ Sh,
+                                                    const bf16x8* __restrict__ gi, float* __restrict__ Q,
+                                                    const int* __restrict__ found) {
+  __shared__ __attribute__((aligned(16))) char lds[Q3Lds<BM>()];
   const int H = g.H, ncb = H / Q3_BN;
   int lid = xcd_swizzle(blockIdx.x, gridDim.x);
   const int cb = lid % ncb;
   lid /= ncb;
   const int q = lid % 4;
   if (found && found[q]) return;
-  const int64_t m0 = (int64_t)(lid / 4) * Q3_BM, BT = g.BT();
+  const int64_t m0 = (int64_t)(lid / 4) * BM, BT = g.BT();
   f32x16 acc[2][4];
-  qgemm3_tile<NP>(g, Sh, gi, q, cb, m0, lds, acc);
+  qgemm3_tile<NP, BM>(g, Sh, gi, q, cb, m0, lds, acc);
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, wr = wave >> 1, wc = wave & 1, c32 = lane & 31;
   float* Qq = Q + (int64_t)q * BT * H + Q3_BN * cb + wc * 128 + c32;
   if constexpr (QP) {
@@ -496,14 +496,22 @@ bool qpair_ok(const Geom& g) { return g.BT() % 4 == 0; }
 
 void launch_qgemm3_img(const Geom& g, const float* Sh, const float* gimg, float* Q, const int* found, hipStream_t s,
                        int pieces, bool qpair) {
-  const int64_t nrt = (g.BT() + Q3_BM - 1) / Q3_BM;
-  dim3 grid((unsigned)(nrt * 4 * (g.H / Q3_BN)));
+  // 128-row tiles, two workgroups per CU.  Q3_BM2=256 (8 waves, half the G-image reads per Q row)
+  // measured slower at C3: 0.54 against 0.48 ms -- the two independent workgroups of a CU drift
+  // out of phase, one staging while the other multiplies, where one workgroup's barriers keep
+  // its waves in step.  (The six-product mode needs 272 registers: one wave per SIMD, 128 rows.)
+#ifndef Q3_BM2
+#define Q3_BM2 128
+#endif
   const bf16x8* gb = reinterpret_cast<const bf16x8*>(gimg);
   qpair = qpair && qpair_ok(g);
-  if (pieces == 2 && qpair) k_qgemm3<2, true><<<grid, kThreads, 0, s>>>(g, Sh, gb, Q, found);
-  else if (pieces == 2) k_qgemm3<2, false><<<grid, kThreads, 0, s>>>(g, Sh, gb, Q, found);
-  else if (qpair) k_qgemm3<3, true><<<grid, kThreads, 0, s>>>(g, Sh, gb, Q, found);
-  else k_qgemm3<3, false><<<grid, kThreads, 0, s>>>(g, Sh, gb, Q, found);
+  const int BM = pieces == 2 ? Q3_BM2 : 128;
+  const int64_t nrt = (g.BT() + BM - 1) / BM;
+  dim3 grid((unsigned)(nrt * 4 * (g.H / Q3_BN)));
+  if (pieces == 2 && qpair) k_qgemm3<2, true, Q3_BM2><<<grid, 2 * Q3_BM2, 0, s>>>(g, Sh, gb, Q, found);
+  else if (pieces == 2) k_qgemm3<2, false, Q3_BM2><<<grid, 2 * Q3_BM2, 0, s>>>(g, Sh, gb, Q, found);
+  else if (qpair) k_qgemm3<3, true, 128><<<grid, 256, 0, s>>>(g, Sh, gb, Q, found);
+  else k_qgemm3<3, false, 128><<<grid, 256, 0, s>>>(g, Sh, gb, Q, found);
 }
 
 void launch_qgemm3(const Geom& g, const float* Sh, const float* G, float* gimg, float* Q, hipStream_t s, int pieces,

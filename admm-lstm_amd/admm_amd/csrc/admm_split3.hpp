@@ -53,25 +53,29 @@ __device__ __forceinline__ void put3(__bf16* img, int piece_stride, int off, f32
 }
 
 // ------------------------------------------------------------------ Q tile = Hprev G
-// Tile: 128 rows x 256 columns of one gate (H % 256 == 0), 4 waves as 2 (rows) x 2 (columns)
-// of 64 x 128; K = H in 16-deep steps through double-buffered LDS, the global loads of step
-// c+1 in flight during the MFMAs of step c.  G comes as the split image of k_split_g:
+// Tile: BM rows x 256 columns of one gate (H % 256 == 0), BM / 32 waves as BM / 64 (rows) x 2
+// (columns) of 64 x 128; K = H in 16-deep steps through double-buffered LDS, the global loads of
+// step c+2 in flight during the MFMAs of step c.  G comes as the split image of k_split_g:
 // gi[(((q * NK + c) * NTT + n) * 3 + p) * 64 + lane] = piece p of the MFMA B fragment of
-// rows 16c.., columns 32n.. (NK = H/16, NTT = H/32).  Ends with a __syncthreads(): the LDS
-// (kQ3Lds bytes from `lds`) is free for the caller's epilogue.
-constexpr int Q3_BM = 128, Q3_BN = 256;
-constexpr int kQ3AP = Q3_BM * 16;               // one piece of the A image (bf16)
+// rows 16c.., columns 32n.. (NK = H/16, NTT = H/32).  Every workgroup reads the G image of its
+// gate (32 KB per step from L2), so BM = 256 halves that traffic per Q row against BM = 128.
+// Ends with a __syncthreads(): the LDS (Q3Lds<BM>() bytes from `lds`) is free for the caller's
+// epilogue.
+constexpr int Q3_BN = 256;
 constexpr int kQ3BU = (Q3_BN / 32) * 3 * 64;    // bf16x8 units of one B step image
-constexpr int kQ3Lds = 2 * 3 * kQ3AP * 2 + 2 * kQ3BU * 16;
+template <int BM>
+constexpr int Q3Lds() { return 2 * 3 * (BM * 16) * 2 + 2 * kQ3BU * 16; }
 
 // NP = 3: the six split3 products (f32-accurate); NP = 2: mfma_split2 (half the matrix work).
-template <int NP>
+template <int NP, int BM>
 __device__ __forceinline__ void qgemm3_tile(const Geom& g, const float* __restrict__ Sh,
                                             const bf16x8* __restrict__ gi, int q, int cb, int64_t m0,
                                             char* lds, f32x16 (&acc)[2][4]) {
   // B image per step: NP = 3 all three pieces of each 32-column tile (192 units), NP = 2 only
   // pieces 0 and 1 (128 units): the third piece is never multiplied there
-  constexpr int AP = kQ3AP, PSTR = NP == 3 ? 192 : 128, BU = (Q3_BN / 32) * PSTR;
+  constexpr int NT = 2 * BM;   // threads
+  constexpr int AP = BM * 16, PSTR = NP == 3 ? 192 : 128, BU = (Q3_BN / 32) * PSTR;
+  static_assert(BU % NT == 0, "B image units per thread");
   __bf16* As = reinterpret_cast<__bf16*>(lds);                       // [2][3 * AP]
   bf16x8* Bs = reinterpret_cast<bf16x8*>(lds + 2 * 3 * AP * 2);       // [2][BU]
   const int H = g.H, NK = H / 16, NTT = H / 32;
@@ -85,7 +89,7 @@ __device__ __forceinline__ void qgemm3_tile(const Geom& g, const float* __restri
   const size_t bstep = (size_t)NTT * 192;
   // two-slot register ring: the loads of step c + 2 are issued at step c (one step of MFMAs does
   // not cover the L2/HBM latency of the next operands); NK is even (H % 256 == 0)
-  struct Slot { float4 a0, a1; bf16x8 b[BU / kThreads]; };
+  struct Slot { float4 a0, a1; bf16x8 b[BU / NT]; };
   auto gload = [&](Slot& r, int c) {
     if (c >= NK) return;
     if (S3_ABL & 32) {
@@ -95,8 +99,8 @@ __device__ __forceinline__ void qgemm3_tile(const Geom& g, const float* __restri
       r.a1 = *reinterpret_cast<const float4*>(ap + 16 * c + 4);
     }
 #pragma unroll
-    for (int u = 0; u < BU / kThreads; ++u) {
-      const int i = tid + u * kThreads;   // image unit -> G-image unit (skipping piece 2 for NP = 2)
+    for (int u = 0; u < BU / NT; ++u) {
+      const int i = tid + u * NT;   // image unit -> G-image unit (skipping piece 2 for NP = 2)
       const int src = NP == 3 ? i : (i >> 7) * 192 + (i & 127);
       r.b[u] = bp[c * bstep + src - tid];
     }
@@ -104,7 +108,7 @@ __device__ __forceinline__ void qgemm3_tile(const Geom& g, const float* __restri
   auto lstore = [&](int st, const Slot& r) {
     put3<NP>(As + st * 3 * AP, AP, sw_off(sr, sh), f32x8{r.a0.x, r.a0.y, r.a0.z, r.a0.w, r.a1.x, r.a1.y, r.a1.z, r.a1.w});
 #pragma unroll
-    for (int u = 0; u < BU / kThreads; ++u) Bs[st * BU + tid + u * kThreads] = r.b[u];
+    for (int u = 0; u < BU / NT; ++u) Bs[st * BU + tid + u * NT] = r.b[u];
   };
   const int wr = wave >> 1, wc = wave & 1, c32 = lane & 31, kh = lane >> 5;
   auto compute = [&](int st) {

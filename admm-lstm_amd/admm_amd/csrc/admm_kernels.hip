@@ -1261,6 +1261,9 @@ __device__ __forceinline__ void trial_point(bool valid, float z, float tg, float
 // pair; they are folded into acc at the end of the pass.
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 constexpr int kPair = kPolyN + 1;
+__device__ __forceinline__ f32x2 fma2(f32x2 a, f32x2 b, f32x2 c) {   // v_pk_fma_f32
+  return f32x2{fmaf(a.x, b.x, c.x), fmaf(a.y, b.y, c.y)};
+}
 
 template <bool TANH>
 __device__ __forceinline__ void trial_pair(bool ok, f32x2 z, f32x2 tg, f32x2 qv, int pass, float (&acc)[kSlots],
@@ -1307,20 +1310,22 @@ __device__ __forceinline__ void trial_pair(bool ok, f32x2 z, f32x2 tg, f32x2 qv,
   acc2[0] += d0 * d0;
   const bool px = fabsf(qv.x) <= kPolyQ, py = fabsf(qv.y) <= kPolyQ;
   if (pass == 0) {
+    // the same ten sums as fma chains into the accumulators, with b_n = 2 a_n (24 instead of
+    // ~30 packed operations per pair; the rounding of each sum's terms differs in the last bit)
     const f32x2 qp = f32x2{px ? qv.x : 0.f, py ? qv.y : 0.f};
     const f32x2 q2 = qp * qp;
     const f32x2 a1 = c1 * qp, a2 = c2 * q2, a3 = c3 * q2 * qp, a4 = c4 * q2 * q2, a5 = c5 * q2 * q2 * qp;
-    const f32x2 t = 2.f * d0;
-    acc2[1] += t * a1;
-    acc2[2] += t * a2 + a1 * a1;
-    acc2[3] += t * a3 + 2.f * a1 * a2;
-    acc2[4] += t * a4 + 2.f * a1 * a3 + a2 * a2;
-    acc2[5] += t * a5 + 2.f * (a1 * a4 + a2 * a3);
-    acc2[6] += 2.f * (a1 * a5 + a2 * a4) + a3 * a3;
-    acc2[7] += 2.f * (a2 * a5 + a3 * a4);
-    acc2[8] += 2.f * a3 * a5 + a4 * a4;
-    acc2[9] += 2.f * a4 * a5;
-    acc2[10] += a5 * a5;
+    const f32x2 t = 2.f * d0, b1 = 2.f * a1, b2 = 2.f * a2, b3 = 2.f * a3, b4 = 2.f * a4;
+    acc2[1] = fma2(t, a1, acc2[1]);
+    acc2[2] = fma2(a1, a1, fma2(t, a2, acc2[2]));
+    acc2[3] = fma2(b1, a2, fma2(t, a3, acc2[3]));
+    acc2[4] = fma2(a2, a2, fma2(b1, a3, fma2(t, a4, acc2[4])));
+    acc2[5] = fma2(b2, a3, fma2(b1, a4, fma2(t, a5, acc2[5])));
+    acc2[6] = fma2(a3, a3, fma2(b2, a4, fma2(b1, a5, acc2[6])));
+    acc2[7] = fma2(b3, a4, fma2(b2, a5, acc2[7]));
+    acc2[8] = fma2(a4, a4, fma2(b3, a5, acc2[8]));
+    acc2[9] = fma2(b4, a5, acc2[9]);
+    acc2[10] = fma2(a5, a5, acc2[10]);
   }
   // per-candidate elements: sigma(w + e) - sigma(w) form (see trial_point)
   const f32x2 f2sg = f32x2{(TANH ? 2.f : 1.f) * (z.x >= 0.f ? 1.f : -1.f), (TANH ? 2.f : 1.f) * (z.y >= 0.f ? 1.f : -1.f)};

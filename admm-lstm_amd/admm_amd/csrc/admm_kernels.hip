@@ -1107,8 +1107,14 @@ __global__ __launch_bounds__(kThreads) void k_qgemm(Geom g, const float* x, cons
 constexpr int kSlots = kTrialSlots;
 constexpr int kSlotPoly = kTrialJ, kSlotFw = kTrialJ + kPolyN, kSlotNne = kTrialJ + kPolyN + 1;
 
-__device__ __forceinline__ void direct_candidates(float cr, float e, float E, float w, float d2,
-                                                  float (&acc)[kSlots]) {
+// sw = f2 sg w (the pushed entry): w = |z| (sigmoid) or 2|z| (tanh) with the sign of z; E and
+// r = sigma(w) are re-formed here exactly as trial_point / trial_pair formed them
+template <bool TANH>
+__device__ __forceinline__ void direct_candidates(float sw, float e, float d2, float (&acc)[kSlots]) {
+  const float w = fabsf(sw);
+  const float E = __expf(-w);
+  const float r = __builtin_amdgcn_rcpf(1.f + E);
+  const float cr = -(sw >= 0.f ? (TANH ? 2.f : 1.f) : (TANH ? -2.f : -1.f)) * r;
   constexpr float kCap = 1e30f;
   float m = fminf(expm1_acc(-e), kCap);
   const float one_e = 1.f + E;
@@ -1144,24 +1150,25 @@ struct DirectQ {
   // the pushes (ds_write) and the run's reads (ds_read) of other lanes' entries address the same
   // array, so they stay in program order, and a wave's LDS operations execute in order: no
   // memory fence (a fence would also order, and so de-scalarise, the caller's global loads)
-  float* buf;              // this wave's [5][kDQ] in LDS
+  float* buf;              // this wave's [3][kDQ] in LDS
   int head, tail;          // wave-uniform counters
 };
 
-__device__ __forceinline__ void dq_push(DirectQ& dq, bool p, float cr, float e, float E, float w, float d2) {
+// An entry is (sw, e, d2): sw = the signed w (E, r and the sign are re-formed from it when the
+// entry runs, one v_exp and one v_rcp per 64 entries instead of two more LDS words per push).
+__device__ __forceinline__ void dq_push(DirectQ& dq, bool p, float sw, float e, float d2) {
   const unsigned long long m = __ballot(p);
   if (p) {
     const int lane = threadIdx.x & 63;
     const int slot = (dq.tail + __popcll(m & ((1ull << lane) - 1ull))) & (kDQ - 1);
-    dq.buf[slot] = cr;
+    dq.buf[slot] = sw;
     dq.buf[kDQ + slot] = e;
-    dq.buf[2 * kDQ + slot] = E;
-    dq.buf[3 * kDQ + slot] = w;
-    dq.buf[4 * kDQ + slot] = d2;
+    dq.buf[2 * kDQ + slot] = d2;
   }
   dq.tail += __popcll(m);
 }
 
+template <bool TANH>
 __device__ __forceinline__ void dq_run(DirectQ& dq, float (&acc)[kSlots], bool final) {
   while (dq.tail - dq.head >= 64 || (final && dq.tail > dq.head)) {
     __builtin_amdgcn_wave_barrier();
@@ -1169,8 +1176,7 @@ __device__ __forceinline__ void dq_run(DirectQ& dq, float (&acc)[kSlots], bool f
     const int n = dq.tail - dq.head < 64 ? dq.tail - dq.head : 64;
     if (lane < n) {
       const int slot = (dq.head + lane) & (kDQ - 1);
-      direct_candidates(dq.buf[slot], dq.buf[kDQ + slot], dq.buf[2 * kDQ + slot], dq.buf[3 * kDQ + slot],
-                        dq.buf[4 * kDQ + slot], acc);
+      direct_candidates<TANH>(dq.buf[slot], dq.buf[kDQ + slot], dq.buf[2 * kDQ + slot], acc);
     }
     dq.head += n;
   }
@@ -1193,7 +1199,7 @@ template <bool TANH>
 __device__ __forceinline__ void trial_point(bool valid, float z, float tg, float qv, int pass, float (&acc)[kSlots],
                                             DirectQ& dq) {
   bool direct = false;
-  float cr = 0.f, e = 0.f, E = 0.f, w = 0.f, d2 = 0.f;
+  float e = 0.f, E = 0.f, w = 0.f, d2 = 0.f;
   if (valid) {
     // E = exp(-w), r = sigma(w), sc = 1 - sigma(w) on w = |z| (sigmoid) or 2|z| (tanh)
     w = TANH ? 2.f * fabsf(z) : fabsf(z);
@@ -1246,12 +1252,11 @@ __device__ __forceinline__ void trial_point(bool valid, float z, float tg, float
       acc[kSlotNne] += 1.f;
       const float sg = z >= 0.f ? 1.f : -1.f;
       const float f2 = TANH ? 2.f : 1.f;
-      cr = -(f2 * sg) * r;
       e = (f2 * sg) * qv * ldexpf(1.f, -(pass * kTrialJ + kTrialJ - 1));   // smallest candidate
       d2 = 2.f * d0;
     }
   }
-  dq_push(dq, direct, cr, e, E, w, d2);
+  dq_push(dq, direct, z >= 0.f ? w : -w, e, d2);
 }
 
 // Two elements of a trial pass at once (the fast path's float4 halves), in packed f32
@@ -1332,8 +1337,8 @@ __device__ __forceinline__ void trial_pair(bool ok, f32x2 z, f32x2 tg, f32x2 qv,
   const float s0 = ldexpf(1.f, -(pass * kTrialJ + kTrialJ - 1));   // smallest candidate
   const bool dx = ok && !px, dy = ok && ok_y && !py;
   acc[kSlotNne] += (dx ? 1.f : 0.f) + (dy ? 1.f : 0.f);
-  dq_push(dq, dx, -f2sg.x * r.x, f2sg.x * qv.x * s0, E.x, w.x, 2.f * d0.x);
-  dq_push(dq, dy, -f2sg.y * r.y, f2sg.y * qv.y * s0, E.y, w.y, 2.f * d0.y);
+  dq_push(dq, dx, z.x >= 0.f ? w.x : -w.x, f2sg.x * qv.x * s0, 2.f * d0.x);
+  dq_push(dq, dy, z.y >= 0.f ? w.y : -w.y, f2sg.y * qv.y * s0, 2.f * d0.y);
 }
 
 __device__ __forceinline__ void trial_pair_fold(float (&acc)[kSlots], const f32x2 (&acc2)[kPair]) {
@@ -1379,14 +1384,14 @@ __device__ __forceinline__ void trial_loop(int64_t n, const float* zq, const flo
         const float tu = u == 0 ? t4.x : (u == 1 ? t4.y : (u == 2 ? t4.z : t4.w));
         const float qu = u == 0 ? q4.x : (u == 1 ? q4.y : (u == 2 ? q4.z : q4.w));
         trial_point<TANH>(ok, zu, tu, qu, pass, acc, dq);
-        dq_run(dq, acc, false);
+        dq_run<TANH>(dq, acc, false);
       }
     } else {
       trial_point<TANH>(ok, ok ? zq[v] : 0.f, ok ? tq[v] : 0.f, ok ? Qq[v] : 0.f, pass, acc, dq);
-      dq_run(dq, acc, false);
+      dq_run<TANH>(dq, acc, false);
     }
   }
-  dq_run(dq, acc, true);
+  dq_run<TANH>(dq, acc, true);
 }
 
 __global__ __launch_bounds__(kThreads) void k_trial(Geom g, int pass, const float* zc, const float* tgt,
@@ -1400,7 +1405,7 @@ __global__ __launch_bounds__(kThreads) void k_trial(Geom g, int pass, const floa
   float acc[kSlots];
 #pragma unroll
   for (int k = 0; k < kSlots; ++k) acc[k] = 0.f;
-  __shared__ float dqbuf[kThreads / 64][5 * kDQ];
+  __shared__ float dqbuf[kThreads / 64][3 * kDQ];
   DirectQ dq{dqbuf[threadIdx.x >> 6], 0, 0};
   const bool vec = (g.H % 4) == 0;
   if (q == 2) {
@@ -1551,14 +1556,14 @@ __device__ __forceinline__ void trial_fast_body(const Geom& g, int q, int pass, 
       acc[1] += cur.z.z * cur.t.z + q4.z + cur.z.w * cur.t.w + q4.w;
     } else {
       trial_pair<TANH>(ok, f32x2{cur.z.x, cur.z.y}, f32x2{cur.t.x, cur.t.y}, f32x2{q4.x, q4.y}, pass, acc, acc2, dq);
-      if (!(TF_ABL & 4)) dq_run(dq, acc, false);
+      if (!(TF_ABL & 4)) dq_run<TANH>(dq, acc, false);
       trial_pair<TANH>(ok, f32x2{cur.z.z, cur.z.w}, f32x2{cur.t.z, cur.t.w}, f32x2{q4.z, q4.w}, pass, acc, acc2, dq);
-      if (!(TF_ABL & 4)) dq_run(dq, acc, false);
+      if (!(TF_ABL & 4)) dq_run<TANH>(dq, acc, false);
     }
     cur = nxt;
   }
   trial_pair_fold(acc, acc2);
-  dq_run(dq, acc, true);
+  dq_run<TANH>(dq, acc, true);
 }
 
 // Wsrc: side 0 -> G_x [4][D][H]; side 1 -> unused (Q holds the h-side direction)
@@ -1576,7 +1581,7 @@ __global__ __launch_bounds__(kThreads, TF_MINB) void k_trial_fast(Geom g, int pa
   float acc[kSlots];
 #pragma unroll
   for (int k = 0; k < kSlots; ++k) acc[k] = 0.f;
-  __shared__ float dqbuf[kThreads / 64][5 * kDQ];
+  __shared__ float dqbuf[kThreads / 64][3 * kDQ];
   DirectQ dq{dqbuf[threadIdx.x >> 6], 0, 0};
   if (q == 2) trial_fast_body<true, SIDE, DP, XV, UR>(g, q, pass, zc, tgt, Q, x, wlds, blk, nblk, acc, dq);
   else trial_fast_body<false, SIDE, DP, XV, UR>(g, q, pass, zc, tgt, Q, x, wlds, blk, nblk, acc, dq);
@@ -1663,12 +1668,12 @@ __device__ __forceinline__ void trial_rows_body(const Geom& g, int q, int pass, 
         const bool ok1 = base + 2 * h + 1 < BT;
         trial_pair<TANH>(true, cur.z[h], ok1 ? cur.t[h] : f32x2{cur.t[h].x, 0.f},
                          ok1 ? cur.q[h] : f32x2{cur.q[h].x, 0.f}, pass, acc, acc2, dq, ok1);
-        dq_run(dq, acc, false);
+        dq_run<TANH>(dq, acc, false);
       }
       cur = nxt;
     }
     trial_pair_fold(acc, acc2);
-    dq_run(dq, acc, true);
+    dq_run<TANH>(dq, acc, true);
     return;
   }
   struct In { f32x2 z, t, q; float xa[DP], xb[DP]; };
@@ -1725,11 +1730,11 @@ __device__ __forceinline__ void trial_rows_body(const Geom& g, int q, int pass, 
     const bool ok1 = base + 1 < BT;
     trial_pair<TANH>(true, cur.z, ok1 ? cur.t : f32x2{cur.t.x, 0.f},
                      ok1 ? qv : f32x2{qv.x, 0.f}, pass, acc, acc2, dq, ok1);
-    dq_run(dq, acc, false);
+    dq_run<TANH>(dq, acc, false);
     cur = nxt;
   }
   trial_pair_fold(acc, acc2);
-  dq_run(dq, acc, true);
+  dq_run<TANH>(dq, acc, true);
 }
 
 template <int SIDE, int DP, bool XV, bool SPEC, bool QP = false>
@@ -1743,7 +1748,7 @@ __global__ __launch_bounds__(kThreads) void k_trial_rows(Geom g, int pass, const
   float acc[kSlots];
 #pragma unroll
   for (int k = 0; k < kSlots; ++k) acc[k] = 0.f;
-  __shared__ float dqbuf[kThreads / 64][5 * kDQ];
+  __shared__ float dqbuf[kThreads / 64][3 * kDQ];
   __shared__ float4 dwl[SPEC ? DP / 4 * 256 : 1];
   DirectQ dq{dqbuf[threadIdx.x >> 6], 0, 0};
   if (q == 2) trial_rows_body<true, SIDE, DP, XV, SPEC, QP>(g, q, pass, zc, tgt, Q, x, Gx, blk, nblk, acc, dq, sp, dwl);
@@ -1848,12 +1853,12 @@ __device__ __forceinline__ void trial_mx_body(const Geom& g, int q, int pass, co
     for (int v = 0; v < 4; ++v) {   // the two columns of row 4 (lane / 16) + v
       const bool ok = row0 + 4 * (lane >> 4) + v < BT;
       trial_pair<TANH>(ok, zv[v], tv[v], f32x2{qa[0][v], qa[1][v]}, pass, acc, acc2, dq, ok);
-      dq_run(dq, acc, false);
+      dq_run<TANH>(dq, acc, false);
     }
     if (TMX_PREFETCH) cur = nxt;
   }
   trial_pair_fold(acc, acc2);
-  dq_run(dq, acc, true);
+  dq_run<TANH>(dq, acc, true);
 }
 
 #ifndef TMX_MINB
@@ -1869,7 +1874,7 @@ __global__ __launch_bounds__(kThreads, TMX_MINB) void k_trial_mx(Geom g, int pas
   float acc[kSlots];
 #pragma unroll
   for (int k = 0; k < kSlots; ++k) acc[k] = 0.f;
-  __shared__ float dqbuf[kThreads / 64][5 * kDQ];
+  __shared__ float dqbuf[kThreads / 64][3 * kDQ];
   DirectQ dq{dqbuf[threadIdx.x >> 6], 0, 0};
   if (q == 2) trial_mx_body<true, SPEC>(g, q, pass, zc, tgt, x, Gx, blk, nblk, acc, dq, sp);
   else trial_mx_body<false, SPEC>(g, q, pass, zc, tgt, x, Gx, blk, nblk, acc, dq, sp);
@@ -2015,10 +2020,10 @@ __device__ __forceinline__ void trial_pair_loop(int64_t n, const float* z, const
     const f32x2 tt = f32x2{ok ? tgt[2 * v] : 0.f, oky ? tgt[2 * v + 1] : 0.f};
     const f32x2 qq = f32x2{ok ? qv[2 * v] : 0.f, oky ? qv[2 * v + 1] : 0.f};
     trial_pair<TANH>(ok, zz, tt, qq, pass, acc, acc2, dq, oky);
-    dq_run(dq, acc, false);
+    dq_run<TANH>(dq, acc, false);
   }
   trial_pair_fold(acc, acc2);
-  dq_run(dq, acc, true);
+  dq_run<TANH>(dq, acc, true);
 }
 
 // Test hook: the same per-element arithmetic on caller data (one gate), kbase = pass*J:
@@ -2034,7 +2039,7 @@ __global__ __launch_bounds__(kThreads) void k_trial_debug(int64_t n, int mode, i
   const int pass = kbase / kTrialJ;
   const bool tanh_gate = mode & 1, pair = mode & 2;
   // the polynomial slots are only filled on pass 0: run pass 0 for them, then this pass
-  __shared__ float dqbuf[kThreads / 64][5 * kDQ];
+  __shared__ float dqbuf[kThreads / 64][3 * kDQ];
   DirectQ dq{dqbuf[threadIdx.x >> 6], 0, 0};
   auto run = [&](int ps, float (&a)[kSlots]) {
     if (pair) {

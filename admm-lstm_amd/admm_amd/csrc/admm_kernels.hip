@@ -1278,18 +1278,21 @@ __device__ __forceinline__ void trial_pair(bool ok, f32x2 z, f32x2 tg, f32x2 qv,
   const f32x2 E = f32x2{__expf(-w.x), __expf(-w.y)};
   const f32x2 r = f32x2{__builtin_amdgcn_rcpf(1.f + E.x), __builtin_amdgcn_rcpf(1.f + E.y)};
   const f32x2 sc = E * r;
-  f32x2 d0, c1, c2, c3, c4, c5;
+  // Taylor coefficients c_n = phi^(n)(z) / n! in factored form: with the trial direction q,
+  // a_n = c_n q^n is a1 = c1 q, a2 = a1 (g2 q), a3 = a1 q^2 k3, a4 = a1 q^2 (g2 q) k4,
+  // a5 = a1 q^4 k5 (trial_point has the c_n themselves)
+  f32x2 d0, c1, g2, k3, k4, k5;
   if (TANH) {
     const f32x2 mz = 2.f * sc;                    // 1 - |tanh z|
     const f32x2 um = 1.f - mz;
     const f32x2 u = f32x2{copysignf(um.x, z.x), copysignf(um.y, z.y)};
     const f32x2 v = mz * (2.f - mz);              // 1 - u^2
     const f32x2 u2 = u * u;
-    c1 = v;
-    c2 = -u * v;
-    c3 = v * (u2 - (1.f / 3.f));
-    c4 = u * v * (2.f - 3.f * u2) * (1.f / 3.f);
-    c5 = v * (2.f - 15.f * u2 * v) * (1.f / 15.f);
+    c1 = v;                                       // c2 = -u v, c3 = v (u^2 - 1/3),
+    g2 = -u;                                      // c4 = u v (2 - 3 u^2) / 3,
+    k3 = u2 - (1.f / 3.f);                        // c5 = v (2 - 15 u^2 v) / 15
+    k4 = u2 - (2.f / 3.f);
+    k5 = fma2(-u2, v, f32x2{2.f / 15.f, 2.f / 15.f});
     // |tanh z| = -expm1(-w) r: degree-8 Taylor of expm1 on |w| < 1/2, else exp - 1
     const f32x2 xm = -w;
     f32x2 pe = 1.f / 40320.f;
@@ -1303,11 +1306,11 @@ __device__ __forceinline__ void trial_pair(bool ok, f32x2 z, f32x2 tg, f32x2 qv,
     const f32x2 sg = f32x2{z.x >= 0.f ? r.x : sc.x, z.y >= 0.f ? r.y : sc.y};   // sigma(z)
     const f32x2 sgc = f32x2{z.x >= 0.f ? sc.x : r.x, z.y >= 0.f ? sc.y : r.y};  // 1 - sigma(z)
     const f32x2 p = sg * sgc, h = sgc - sg;
-    c1 = p;
-    c2 = 0.5f * p * h;
-    c3 = p * (1.f - 6.f * p) * (1.f / 6.f);
-    c4 = p * h * (1.f - 12.f * p) * (1.f / 24.f);
-    c5 = p * (1.f - 30.f * p + 120.f * p * p) * (1.f / 120.f);
+    c1 = p;                                       // c2 = p h / 2, c3 = p (1 - 6p) / 6,
+    g2 = 0.5f * h;                                // c4 = p h (1 - 12p) / 24,
+    k3 = (1.f / 6.f) - p;                         // c5 = p (1 - 30p + 120p^2) / 120
+    k4 = (1.f / 12.f) - p;
+    k5 = fma2(p, p - 0.25f, f32x2{1.f / 120.f, 1.f / 120.f});
     d0 = sg - tg;
   }
   const f32x2 okm = f32x2{ok ? 1.f : 0.f, ok && ok_y ? 1.f : 0.f};
@@ -1318,8 +1321,9 @@ __device__ __forceinline__ void trial_pair(bool ok, f32x2 z, f32x2 tg, f32x2 qv,
     // the same ten sums as fma chains into the accumulators, with b_n = 2 a_n (24 instead of
     // ~30 packed operations per pair; the rounding of each sum's terms differs in the last bit)
     const f32x2 qp = f32x2{px ? qv.x : 0.f, py ? qv.y : 0.f};
-    const f32x2 q2 = qp * qp;
-    const f32x2 a1 = c1 * qp, a2 = c2 * q2, a3 = c3 * q2 * qp, a4 = c4 * q2 * q2, a5 = c5 * q2 * q2 * qp;
+    const f32x2 q2 = qp * qp, gq = g2 * qp;
+    const f32x2 a1 = c1 * qp, a2 = a1 * gq, w3 = a1 * q2;
+    const f32x2 a3 = w3 * k3, a4 = (w3 * gq) * k4, a5 = (w3 * q2) * k5;
     const f32x2 t = 2.f * d0, b1 = 2.f * a1, b2 = 2.f * a2, b3 = 2.f * a3, b4 = 2.f * a4;
     acc2[1] = fma2(t, a1, acc2[1]);
     acc2[2] = fma2(a1, a1, fma2(t, a2, acc2[2]));

@@ -1168,8 +1168,11 @@ __device__ __forceinline__ void dq_push(DirectQ& dq, bool p, float sw, float e, 
   dq.tail += __popcll(m);
 }
 
+// final: also counts the wave's per-candidate elements (every push, in lane 0's slot) -- the
+// number of elements the pass could not cover with the polynomial (k_select's poly_only test)
 template <bool TANH>
 __device__ __forceinline__ void dq_run(DirectQ& dq, float (&acc)[kSlots], bool final) {
+  if (final && (threadIdx.x & 63) == 0) acc[kSlotNne] += (float)dq.tail;
   while (dq.tail - dq.head >= 64 || (final && dq.tail > dq.head)) {
     __builtin_amdgcn_wave_barrier();
     const int lane = threadIdx.x & 63;
@@ -1249,7 +1252,6 @@ __device__ __forceinline__ void trial_point(bool valid, float z, float tg, float
       }
     } else {
       direct = true;
-      acc[kSlotNne] += 1.f;
       const float sg = z >= 0.f ? 1.f : -1.f;
       const float f2 = TANH ? 2.f : 1.f;
       e = (f2 * sg) * qv * ldexpf(1.f, -(pass * kTrialJ + kTrialJ - 1));   // smallest candidate
@@ -1340,7 +1342,6 @@ __device__ __forceinline__ void trial_pair(bool ok, f32x2 z, f32x2 tg, f32x2 qv,
   const f32x2 f2sg = f32x2{(TANH ? 2.f : 1.f) * (z.x >= 0.f ? 1.f : -1.f), (TANH ? 2.f : 1.f) * (z.y >= 0.f ? 1.f : -1.f)};
   const float s0 = ldexpf(1.f, -(pass * kTrialJ + kTrialJ - 1));   // smallest candidate
   const bool dx = ok && !px, dy = ok && ok_y && !py;
-  acc[kSlotNne] += (dx ? 1.f : 0.f) + (dy ? 1.f : 0.f);
   dq_push(dq, dx, z.x >= 0.f ? w.x : -w.x, f2sg.x * qv.x * s0, 2.f * d0.x);
   dq_push(dq, dy, z.y >= 0.f ? w.y : -w.y, f2sg.y * qv.y * s0, 2.f * d0.y);
 }

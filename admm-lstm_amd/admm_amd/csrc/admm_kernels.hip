@@ -1157,10 +1157,11 @@ struct DirectQ {
 // An entry is (sw, e, d2): sw = the signed w (E, r and the sign are re-formed from it when the
 // entry runs, one v_exp and one v_rcp per 64 entries instead of two more LDS words per push).
 __device__ __forceinline__ void dq_push(DirectQ& dq, bool p, float sw, float e, float d2) {
-  const unsigned long long m = __ballot(p);
+  const unsigned long long m = __builtin_amdgcn_ballot_w64(p);
   if (p) {
-    const int lane = threadIdx.x & 63;
-    const int slot = (dq.tail + __popcll(m & ((1ull << lane) - 1ull))) & (kDQ - 1);
+    // this lane's rank among the pushing lanes: v_mbcnt_lo / v_mbcnt_hi on the ballot
+    const int rank = __builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
+    const int slot = (dq.tail + rank) & (kDQ - 1);
     dq.buf[slot] = sw;
     dq.buf[kDQ + slot] = e;
     dq.buf[2 * kDQ + slot] = d2;
@@ -1856,7 +1857,7 @@ __device__ __forceinline__ void trial_mx_body(const Geom& g, int q, int pass, co
     }
 #pragma unroll
     for (int v = 0; v < 4; ++v) {   // the two columns of row 4 (lane / 16) + v
-      const bool ok = row0 + 4 * (lane >> 4) + v < BT;
+      const bool ok = (int)row0 + 4 * (lane >> 4) + v < (int)BT;   // 32-bit: trial_mx_ok bounds BT H
       trial_pair<TANH>(ok, zv[v], tv[v], f32x2{qa[0][v], qa[1][v]}, pass, acc, acc2, dq, ok);
       dq_run<TANH>(dq, acc, false);
     }

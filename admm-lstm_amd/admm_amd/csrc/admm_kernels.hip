@@ -1810,8 +1810,7 @@ __device__ __forceinline__ void trial_mx_body(const Geom& g, int q, int pass, co
 #pragma unroll
   for (int k = 0; k < kPair; ++k) acc2[k] = f32x2{0.f, 0.f};
   const int64_t ntile = (BT + 15) / 16;
-  // operands of one tile; the next tile's are loaded while this one is evaluated (rows past
-  // BT clamped: branch-free, masked by ok below)
+  // operands of one tile (rows past BT load 0 through the descriptor and are masked by ok below)
   struct In { float xa[4]; f32x2 zv[4], tv[4]; };
   auto load = [&](int64_t tile, In& v) {
     const uint32_t row0 = (uint32_t)tile * 16;
@@ -1829,18 +1828,29 @@ __device__ __forceinline__ void trial_mx_body(const Geom& g, int q, int pass, co
       v.tv[r] = buf_ld2(rT, o + r * rowb);
     }
   };
-#ifndef TMX_PREFETCH
-#define TMX_PREFETCH 0   // 1: the next tile's operands in registers (needs 3 waves/SIMD, TMX_MINB 3)
+#ifndef TMX_ROLL
+#define TMX_ROLL 1
 #endif
-  In cur, nxt;
-  if (TMX_PREFETCH) load(blk, cur);
+  // TMX_ROLL: a rolling prefetch in the registers of the tile being evaluated -- the next tile's
+  // x operand is loaded once this tile's MFMAs have read theirs, and its row v once trial_pair
+  // has consumed this tile's row v (a tile of latency cover for no extra registers)
+  In cur;
+  const auto load_x = [&](int64_t tile) {
+    const uint32_t xo = (((uint32_t)tile * 16 + (lane & 15)) * g.D + (lane >> 4)) * 4;
+#pragma unroll
+    for (int s4 = 0; s4 < 4; ++s4) {
+      const int d = 4 * s4 + (lane >> 4);
+      cur.xa[s4] = d < g.D ? buf_ld<0>(rX, xo + 16 * s4) : 0.f;
+    }
+  };
+  if (TMX_ROLL) load(blk, cur);
   for (int64_t tile = blk; tile < ntile; tile += nblk) {
     const int64_t row0 = tile * 16;
-    if (TMX_PREFETCH) load(tile + nblk < ntile ? tile + nblk : tile, nxt);
-    else load(tile, cur);
+    const int64_t tn = tile + nblk < ntile ? tile + nblk : tile;
+    if (!TMX_ROLL) load(tile, cur);
     const float (&xa)[4] = cur.xa;
-    const f32x2 (&zv)[4] = cur.zv;
-    const f32x2 (&tv)[4] = cur.tv;
+    f32x2 (&zv)[4] = cur.zv;
+    f32x2 (&tv)[4] = cur.tv;
     f32x4 qa[2] = {}, da[2] = {};
 #pragma unroll
     for (int s4 = 0; s4 < 4; ++s4)
@@ -1855,20 +1865,25 @@ __device__ __forceinline__ void trial_mx_body(const Geom& g, int q, int pass, co
 #pragma unroll
       for (int v = 0; v < 4; ++v) buf_st2(rZX, o + v * rowb, zv[v] + f32x2{da[0][v], da[1][v]});
     }
+    if (TMX_ROLL) load_x(tn);
+    const uint32_t on = (uint32_t)tn * 16 * rowb + lofs;
 #pragma unroll
     for (int v = 0; v < 4; ++v) {   // the two columns of row 4 (lane / 16) + v
       const bool ok = (int)row0 + 4 * (lane >> 4) + v < (int)BT;   // 32-bit: trial_mx_ok bounds BT H
       trial_pair<TANH>(ok, zv[v], tv[v], f32x2{qa[0][v], qa[1][v]}, pass, acc, acc2, dq, ok);
+      if (TMX_ROLL) {
+        zv[v] = buf_ld2(rZ, on + v * rowb);
+        tv[v] = buf_ld2(rT, on + v * rowb);
+      }
       dq_run<TANH>(dq, acc, false);
     }
-    if (TMX_PREFETCH) cur = nxt;
   }
   trial_pair_fold(acc, acc2);
   dq_run<TANH>(dq, acc, true);
 }
 
 #ifndef TMX_MINB
-#define TMX_MINB 4   // 4 waves/SIMD (128 VGPRs) without the register prefetch: 0.88 -> 0.86 ms at C3
+#define TMX_MINB 4   // 4 waves/SIMD (128 VGPRs), the next tile prefetched in place (TMX_ROLL)
 #endif
 template <bool SPEC>
 __global__ __launch_bounds__(kThreads, TMX_MINB) void k_trial_mx(Geom g, int pass, const float* __restrict__ zc,

@@ -328,10 +328,11 @@ constexpr int A3W_THREADS = 512;
 #endif
 struct Atr3wRing { float4 a[2], z[2], t[2]; };
 
+// (mb, nb): the 256 x 256 block of G_q (H_prev columns 256 mb.., R columns 256 nb..)
 template <bool TANH>
-__device__ __forceinline__ void atr3w_body(const Geom& g, int q, int sp, int nsplit, const float* __restrict__ Sh,
-                                           const float* __restrict__ zq, const float* __restrict__ tq,
-                                           float* __restrict__ slab, __bf16* img) {
+__device__ __forceinline__ void atr3w_body(const Geom& g, int q, int sp, int nsplit, int mb, int nb,
+                                           const float* __restrict__ Sh, const float* __restrict__ zq,
+                                           const float* __restrict__ tq, float* __restrict__ slab, __bf16* img) {
   using P = A3<256>;
   const int H = g.H;
   const int64_t BT = g.BT();
@@ -345,6 +346,7 @@ __device__ __forceinline__ void atr3w_body(const Geom& g, int q, int sp, int nsp
   const __amdgpu_buffer_rsrc_t rZ = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(zq), 0, (int)(BT * H * 4), kBufWord3);
   const __amdgpu_buffer_rsrc_t rT = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(tq), 0, (int)(BT * H * 4), kBufWord3);
   const int vo = 16 * lane;   // float4 column 4 lane of a 256-float row
+  const int va = vo + 1024 * mb, vz = vo + 1024 * nb;   // + the block's first column
   auto gload = [&](Atr3wRing& R, int64_t k0) {   // rows past r1 clamped; they meet R = 0 in put()
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
@@ -353,9 +355,9 @@ __device__ __forceinline__ void atr3w_body(const Geom& g, int q, int sp, int nsp
         R.a[i] = make_float4((float)row, 0.5f, 0.25f, 0.125f); R.z[i] = R.a[i]; R.t[i] = R.a[i];
         continue;
       }
-      R.a[i] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rA, vo, (int)(g.hrow(row) * H * 4), 0));
-      R.z[i] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rZ, vo, (int)(row * H * 4), 2));
-      R.t[i] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rT, vo, (int)(row * H * 4), 2));
+      R.a[i] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rA, va, (int)(g.hrow(row) * H * 4), 0));
+      R.z[i] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rZ, vz, (int)(row * H * 4), 2));
+      R.t[i] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rT, vz, (int)(row * H * 4), 2));
     }
   };
   auto put = [&](int st, const Atr3wRing& R, int64_t k0) {
@@ -439,7 +441,7 @@ __device__ __forceinline__ void atr3w_body(const Geom& g, int q, int sp, int nsp
       __syncthreads();
     }
   }
-  float* out = slab + ((int64_t)sp * 4 + q) * H * H + wc * 64 + (lane & 31);
+  float* out = slab + ((int64_t)sp * 4 + q) * H * H + (int64_t)(256 * mb) * H + 256 * nb + wc * 64 + (lane & 31);
 #pragma unroll
   for (int mi = 0; mi < 4; ++mi)
 #pragma unroll
@@ -456,10 +458,11 @@ __global__ __launch_bounds__(A3W_THREADS, 1) void k_atr3w(Geom g, const float* _
   __shared__ __attribute__((aligned(16))) __bf16 img[2 * A3<256>::STAGE];
   int lid = xcd_swizzle(blockIdx.x, gridDim.x);
   const int q = lid % 4;          // the 4 gates of one split share the Hprev rows: same XCD
-  const int sp = lid / 4;
+  lid /= 4;
+  const int nt = g.H / 256, tl = lid % (nt * nt), sp = lid / (nt * nt);
   const int64_t n = g.BT() * g.H;
-  if (q == 2) atr3w_body<true>(g, q, sp, nsplit, Sh, zc + q * n, tgt + q * n, slab, img);
-  else atr3w_body<false>(g, q, sp, nsplit, Sh, zc + q * n, tgt + q * n, slab, img);
+  if (q == 2) atr3w_body<true>(g, q, sp, nsplit, tl / nt, tl % nt, Sh, zc + q * n, tgt + q * n, slab, img);
+  else atr3w_body<false>(g, q, sp, nsplit, tl / nt, tl % nt, Sh, zc + q * n, tgt + q * n, slab, img);
 }
 
 }  // namespace
@@ -478,13 +481,17 @@ int atr3_splits(const Geom& g) {
   return ns < 1 ? 1 : ns;
 }
 
-bool atr3w_ok(const Geom& g) { return g.H == 256; }
+bool atr3w_ok(const Geom& g) { return g.H % 256 == 0; }
 
 void launch_atr3(const Geom& g, const float* Sh, const float* zc, const float* tgt, float* slab, int nsplit,
                  hipStream_t s, bool two_waves) {
   dim3 grid((g.H / A3_BM) * (g.H / A3_BN) * 4 * nsplit);
-  if (two_waves && atr3w_ok(g)) k_atr3w<<<4 * nsplit, A3W_THREADS, 0, s>>>(g, Sh, zc, tgt, slab, nsplit);
-  else k_atr3<<<grid, kThreads, 0, s>>>(g, Sh, zc, tgt, slab, nsplit);
+  if (two_waves && atr3w_ok(g)) {   // 256 x 256 blocks of each gate's G, nsplit row ranges
+    const int nt = g.H / 256;
+    k_atr3w<<<4 * nt * nt * nsplit, A3W_THREADS, 0, s>>>(g, Sh, zc, tgt, slab, nsplit);
+  } else {
+    k_atr3<<<grid, kThreads, 0, s>>>(g, Sh, zc, tgt, slab, nsplit);
+  }
 }
 
 void launch_split_g(const Geom& g, const float* G, float* gimg, hipStream_t s) {

@@ -821,10 +821,11 @@ def test_q_two_piece_split_same_trajectory(shape, mods, dev, monkeypatch):
 
 
 @pytest.mark.parametrize('knob,shape', [('ADMM_ATR3W', (2048, 8, 16, 256)), ('ADMM_ATR3W', (333, 3, 5, 256)),
+                                        ('ADMM_ATR3W', (300, 3, 16, 512)),
                                         ('ADMM_QPAIR', (1000, 5, 16, 256)), ('ADMM_QPAIR', (301, 3, 16, 512)),
                                         ('ADMM_QPAIR', (301, 2, 16, 256))])
 def test_h_stage_layout_knobs_bit_identical(knob, shape, mods, dev, monkeypatch):
-    """ADMM_ATR3W: k_atr3w (8 waves, two per SIMD, the default at H = 256) forms the h-side
+    """ADMM_ATR3W: k_atr3w (8 waves, two per SIMD, the default for H % 256 == 0) forms the h-side
     gradient slabs with the same products in the same order as k_atr3 (one wave per SIMD).
     ADMM_QPAIR: k_qgemm3 stores Q in the row-quad layout that the h-side trials read (default)
     instead of row-major (the same values).  Either way the trajectories must be bitwise equal,

@@ -21,7 +21,9 @@ struct Planes {
   float* G[4];
 };
 
-template <int ROWS, int AHEAD>
+// ZI: the eight library planes (z cache, tgt) interleaved as one [B*T][8][H] buffer (P.Z[0]),
+// so that the 8 stores of one point land in one 8-KB row instead of 8 planes
+template <int ROWS, int AHEAD, bool ZI = false>
 __global__ __launch_bounds__(256) void k_pat(Planes P) {
   constexpr int COLS = 1024 / ROWS, NT = H / COLS, TPR = COLS / 4;
   const int ct = threadIdx.x, row = ct / TPR, c4 = (ct % TPR) * 4;
@@ -57,8 +59,14 @@ __global__ __launch_bounds__(256) void k_pat(Planes P) {
       *reinterpret_cast<f4*>(P.S[4] + o) = acc;
       *reinterpret_cast<f4*>(P.S[5] + o) = acc;
       for (int k = 0; k < 5; ++k) stnt(P.L[k] + o, acc - (float)k);
-      for (int k = 0; k < 4; ++k) stnt(P.Z[k] + e, acc * (float)k);
-      for (int k = 0; k < 4; ++k) stnt(P.G[k] + e, acc * (float)(k + 2));
+      if (ZI) {
+        const int64_t ei = (b * T + (t - 1)) * 8 * H + n * COLS + c4;
+        for (int k = 0; k < 4; ++k) stnt(P.Z[0] + ei + (2 * k) * H, acc * (float)k);
+        for (int k = 0; k < 4; ++k) stnt(P.Z[0] + ei + (2 * k + 1) * H, acc * (float)(k + 2));
+      } else {
+        for (int k = 0; k < 4; ++k) stnt(P.Z[k] + e, acc * (float)k);
+        for (int k = 0; k < 4; ++k) stnt(P.G[k] + e, acc * (float)(k + 2));
+      }
       __syncthreads();
     }
 }
@@ -99,6 +107,8 @@ int main() {
   Planes P;
 #define ATTR(RR, AA) CK(hipFuncSetAttribute((const void*)k_pat<RR, AA>, hipFuncAttributeMaxDynamicSharedMemorySize, 100 * 1024))
   ATTR(32, 1); ATTR(32, 2); ATTR(16, 1); ATTR(16, 2); ATTR(8, 1); ATTR(8, 2); ATTR(4, 1); ATTR(4, 2);
+  CK(hipFuncSetAttribute((const void*)k_pat<32, 1, true>, hipFuncAttributeMaxDynamicSharedMemorySize, 100 * 1024));
+  CK(hipFuncSetAttribute((const void*)k_pat<16, 1, true>, hipFuncAttributeMaxDynamicSharedMemorySize, 100 * 1024));
   const size_t plane = (size_t)B * (T + 1) * H, zpl = (size_t)B * T * H;
   for (int k = 0; k < 6; ++k) {
     CK(hipMalloc(&P.S[k], plane * 4));
@@ -107,7 +117,7 @@ int main() {
     CK(hipMemset(P.L[k], 0, plane * 4));
   }
   for (int k = 0; k < 4; ++k) {
-    CK(hipMalloc(&P.Z[k], zpl * 4));
+    CK(hipMalloc(&P.Z[k], (k == 0 ? 8 : 1) * zpl * 4));   // Z[0] also holds the interleaved image (ZI)
     CK(hipMalloc(&P.G[k], zpl * 4));
   }
   const double bytes = 30.0 * zpl * 4;   // 11 loads + 19 stores per point
@@ -116,6 +126,22 @@ int main() {
   report("seq (1 pass, grid 4096)", timeit([&] { k_seq<<<4096, 256>>>(P, (int64_t)zpl / 4); }, reps));
   report("seq (1 pass, grid 1024)", timeit([&] { k_seq<<<1024, 256>>>(P, (int64_t)zpl / 4); }, reps));
   // dynamic LDS only limits residency: 100 KB -> 1 workgroup (4 waves) per CU, 60 KB -> 2
+  // separate vs interleaved library planes, alternating rounds
+  for (int round = 0; round < 3; ++round)
+    for (int R : {32, 16})
+      for (int zi : {0, 1})
+        for (int lds : {100 * 1024, 60 * 1024, 0}) {
+          char name[96];
+          snprintf(name, sizeof name, "r%d tile %2d rows, %s, %s", round, R, zi ? "z/tgt interleaved" : "z/tgt planes",
+                   lds > 80000 ? "1 WG/CU" : lds ? "2 WG/CU" : "max WG/CU");
+          auto go = [&] {
+            if (R == 32 && zi) k_pat<32, 1, true><<<B / 32, 256, lds>>>(P);
+            if (R == 32 && !zi) k_pat<32, 1><<<B / 32, 256, lds>>>(P);
+            if (R == 16 && zi) k_pat<16, 1, true><<<B / 16, 256, lds>>>(P);
+            if (R == 16 && !zi) k_pat<16, 1><<<B / 16, 256, lds>>>(P);
+          };
+          report(name, timeit(go, reps));
+        }
   for (int R : {32, 16, 8, 4})
     for (int A : {1, 2})
       for (int lds : {100 * 1024, 60 * 1024, 0}) {

@@ -477,6 +477,15 @@ int admm_create(const AdmmDims* dims, const AdmmParams* params, int device, Admm
   if (const char* e = std::getenv("ADMM_Q_PIECES")) c->q_pieces = std::atoi(e) == 2 ? 2 : 3;
   Hyper& h = c->hp;
   for (int i = 0; i < 7; ++i) h.rho[i] = params->rho[i];
+  h.rinv_exact = 1;
+  for (int i = 0; i < 4; ++i) {   // rho = 2^(e-1) with 2^(1-e) a normal float
+    int e = 0;
+    const float m = std::frexp(h.rho[i], &e);
+    const bool p2 = m == 0.5f && 1 - e >= -126 && 1 - e <= 127;
+    h.rinv_gate[i] = p2 ? std::ldexp(1.f, 1 - e) : 0.f;
+    h.rinv_exact &= p2 ? 1 : 0;
+  }
+  if (const char* e = std::getenv("ADMM_RINV")) h.rinv_exact &= std::atoi(e) != 0 ? 1 : 0;
   for (int q = 0; q < 4; ++q) {
     h.beta_x[q] = params->beta_x[q];
     h.beta_h[q] = params->beta_h[q];

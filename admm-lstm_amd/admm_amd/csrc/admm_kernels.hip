@@ -140,6 +140,14 @@ __global__ __launch_bounds__(kThreads) void k_forward_t(Geom g, int t, Weights w
 // admm.py:302-312), written by k_resid_gx or by the persistent sweep: one expression (IEEE
 // division, as the reference) so that either source gives equal bits.
 __device__ __forceinline__ f32x4 tgt_quot(f32x4 lam, float rho, f32x4 s) { return lam / rho + s; }
+// The same value when rho is a power of two (Hyper::rinv_exact): lam * 2^-k is exact, so it
+// equals the correctly rounded quotient; __fmul_rn keeps the product out of an fma with s.
+__device__ __forceinline__ f32x4 tgt_mulq(f32x4 lam, float rinv, f32x4 s) {
+  f32x4 q;
+#pragma unroll
+  for (int u = 0; u < 4; ++u) q[u] = __fmul_rn(lam[u], rinv);
+  return q + s;
+}
 
 // ---- one (b, j) point of the time sweep: i, f, g, o (admm.py:353-386), c (388-436),
 // h for t < T (455-457), duals of i, f, g, o, c (504-530).  Operand grouping follows the
@@ -659,8 +667,14 @@ __global__ __launch_bounds__(SR_THREADS) void k_sweep_rows(Geom g, const bf16x8*
       for (int k = 0; k + 1 < NT; ++k) cring[k] = cring[k + 1];
       cring[NT - 1] = c1;
       // lam/rho + S of the updated i, f, g, o: the next x stage's targets (tgt_quot, as k_resid_gx)
-      const f32x4 ti = tgt_quot(li, hp.rho[0], i1), tf = tgt_quot(lf, hp.rho[1], f1);
-      const f32x4 tg = tgt_quot(lg, hp.rho[2], g1), to = tgt_quot(lo, hp.rho[3], o1);
+      f32x4 ti, tf, tg, to;
+      if (hp.rinv_exact) {   // workgroup-uniform: 16 IEEE divisions per tile and thread saved
+        ti = tgt_mulq(li, hp.rinv_gate[0], i1); tf = tgt_mulq(lf, hp.rinv_gate[1], f1);
+        tg = tgt_mulq(lg, hp.rinv_gate[2], g1); to = tgt_mulq(lo, hp.rinv_gate[3], o1);
+      } else {
+        ti = tgt_quot(li, hp.rho[0], i1); tf = tgt_quot(lf, hp.rho[1], f1);
+        tg = tgt_quot(lg, hp.rho[2], g1); to = tgt_quot(lo, hp.rho[3], o1);
+      }
       if constexpr (GX) {   // R = (phi(z) - tgt) phi'(z) into the z slot (0 past the last row)
         const float m = rok ? 1.f : 0.f;
         Z[0] = (ai - ti) * di * m;

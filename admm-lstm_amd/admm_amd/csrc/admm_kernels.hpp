@@ -57,6 +57,10 @@ struct Hyper {
   float beta_x[4], beta_h[4], beta_y;
   int variant;              // 0 admm, 1 no_dual_y
   int with_dual_y;
+  // 1/rho of gates i, f, g, o when all four rho are powers of two (then lam * (1/rho) is
+  // exact and equals the IEEE quotient lam / rho bit for bit), else 0: tgt_quot's fast form
+  float rinv_gate[4];
+  int rinv_exact;
 };
 
 // Device-side diagnostics, copied out by admm_get_stats.

@@ -589,6 +589,38 @@ def test_lamh_skip_bit_identical(lamh_edit, mods, dev, monkeypatch):
     assert torch.equal(out[0], out[1])
 
 
+@pytest.mark.parametrize('rho_gates', [(1., 1., 1., 1.), (0.5, 2., 0.25, 4.), (1.5, 1., 1., 1.)])
+def test_tgt_reciprocal_bit_identical(rho_gates, mods, dev, monkeypatch):
+    """The persistent sweep forms tgt = lam * (1/rho) + S when the four gate rho are powers of
+    two (exact, so equal to the reference's IEEE quotient lam / rho, admm.py:302-312); against
+    ADMM_RINV=0 (always divide): bit-identical weights, gates and duals over three steps.  The
+    third rho set is not all powers of two and takes the division path both times."""
+    from blocks.lstm import LSTM
+    from parameters import example_parameter_dictionary
+    admm, _ = mods
+    admm.with_dual_y = False
+    B, T, D, H = 300, 4, 16, 256
+    g = torch.Generator().manual_seed(12)
+    x = torch.rand(B, T, D, generator=g).to(dev)
+    y = torch.rand(B, 1, generator=g).to(dev)
+    pd = {'rho': dict(example_parameter_dictionary['GoogleStock']['rho']),
+          'beta': dict(example_parameter_dictionary['GoogleStock']['beta'])}
+    pd['rho'].update(zip('ifgo', rho_gates))
+    out = []
+    for flag in ('1', '0'):
+        monkeypatch.setenv('ADMM_RINV', flag)
+        torch.manual_seed(0)
+        m = LSTM(D, H, 1).to(dev)
+        opt = admm.ADMMBasedOptimizer(m, (x, y), pd, verbose=False)
+        for _ in range(3):
+            opt.step()
+        out.append(torch.cat([p.detach().flatten() for p in m.parameters()]
+                             + [v.flatten() for v in opt.gates.values()] + [v.flatten() for v in opt.duals.values()]))
+        del opt
+    assert torch.isfinite(out[0]).all()
+    assert torch.equal(out[0], out[1])
+
+
 def test_split3_h_stage_matches_f32_mfma(mods, dev, monkeypatch):
     """The h-stage GEMMs on split bf16 MFMAs (admm_split3.hip, used when H % 256 == 0) agree
     with the f32-MFMA kernels (ADMM_SPLIT3=0) on a C3-shaped problem (H = 256, D = 16) over

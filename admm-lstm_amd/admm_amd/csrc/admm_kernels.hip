@@ -2158,7 +2158,18 @@ __global__ __launch_bounds__(kThreads) void k_select(Geom g, Hyper hp, SelectArg
 #pragma unroll
     for (int k = 0; k < kSlots; ++k) acc[k] = 0.0;
     const double* p = a.part + (int64_t)q * kSlots * a.nred;
-    for (int i = tid; i < a.nred; i += kThreads) {
+    int i = tid;
+    for (; i + kThreads < a.nred; i += 2 * kThreads) {   // two partials' loads in flight, same sum order
+      double v0[kSlots], v1[kSlots];
+#pragma unroll
+      for (int k = 0; k < kSlots; ++k) {
+        v0[k] = p[(int64_t)k * a.nred + i];
+        v1[k] = p[(int64_t)k * a.nred + i + kThreads];
+      }
+#pragma unroll
+      for (int k = 0; k < kSlots; ++k) acc[k] = (acc[k] + v0[k]) + v1[k];
+    }
+    if (i < a.nred) {
 #pragma unroll
       for (int k = 0; k < kSlots; ++k) acc[k] += p[(int64_t)k * a.nred + i];
     }
@@ -2181,6 +2192,15 @@ __global__ __launch_bounds__(kThreads) void k_select(Geom g, Hyper hp, SelectArg
     const float4* G4 = reinterpret_cast<const float4*>(Gq);
     const int64_t n4 = nW / 4;
     int64_t i = tid;
+    // two groups of 8 loads in flight; the sum order is the 8-at-a-time loop's
+    for (; i + 15 * kThreads < n4; i += 16 * kThreads) {
+      float4 v[16];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) v[u] = G4[i + u * kThreads];
+#pragma unroll
+      for (int u = 0; u < 16; ++u)
+        gs += ((double)v[u].x * v[u].x + (double)v[u].y * v[u].y) + ((double)v[u].z * v[u].z + (double)v[u].w * v[u].w);
+    }
     for (; i + 7 * kThreads < n4; i += 8 * kThreads) {
       float4 v[8];
 #pragma unroll
@@ -2247,7 +2267,20 @@ __global__ __launch_bounds__(kThreads) void k_select(Geom g, Hyper hp, SelectArg
   const float beta = a.side == 0 ? hp.beta_x[q] : hp.beta_h[q];
   const WUpd u = WUpd::make(rho, beta, g.T, pick);
   float* W = a.W[q];
-  for (int64_t i = (int64_t)mb * kThreads + tid; i < nW; i += (int64_t)gridDim.x * kThreads) {
+  const int64_t gstride = (int64_t)gridDim.x * kThreads;
+  int64_t i = (int64_t)mb * kThreads + tid;
+  for (; i + 3 * gstride < nW; i += 4 * gstride) {   // four elements' loads in flight
+    float w0[4], gv[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) { w0[e] = W[i + e * gstride]; gv[e] = Gq[i + e * gstride]; }
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float w1 = u.apply(w0[e], gv[e]);
+      W[i + e * gstride] = w1;
+      if (a.dW) a.dW[(int64_t)q * nW + i + e * gstride] = w1 - w0[e];
+    }
+  }
+  for (; i < nW; i += gstride) {
     const float w0 = W[i];
     const float w1 = u.apply(w0, Gq[i]);
     W[i] = w1;

@@ -2405,7 +2405,7 @@ __device__ __forceinline__ float ht_grad(const Geom& g, const Hyper& hp, const H
 }
 
 template <int OC>
-__global__ __launch_bounds__(kThreads) void k_ht_partial(Geom g, Hyper hp, Planes6 S, Planes6 L, const float* a,
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(8))) void k_ht_partial(Geom g, Hyper hp, Planes6 S, Planes6 L, const float* a,
                                                            const float* Ly, const float* wy, double* part) {
   const int NO = OC > 0 ? OC : g.O;   // output width: compile-time for O = 1 (arrays stay in registers)
   __shared__ double red[4];
@@ -2415,8 +2415,11 @@ __global__ __launch_bounds__(kThreads) void k_ht_partial(Geom g, Hyper hp, Plane
   const bool nd = hp.variant == 1;
   const bool shift = !nd && hp.with_dual_y;
   const int64_t rs = (int64_t)g.TP() * g.H, tofs = (int64_t)g.T * g.H;
-  double acc[kHTSums];
-  for (int i = 0; i < kHTSums; ++i) acc[i] = 0.0;
+  // the wave's running sums live in LDS (lane 0 adds, same order as registers would): 26 VGPRs
+  // fewer, so all C3 rows' waves are resident at once
+  double* acc = accs[w];
+  if (lane == 0)
+    for (int i = 0; i < kHTSums; ++i) acc[i] = 0.0;
   float sbuf[HT_W];
   for (int64_t b = (int64_t)blockIdx.x * 4 + w; b < g.B; b += (int64_t)gridDim.x * 4) {
     const float* h = S.p[5] + b * rs + tofs;
@@ -2447,7 +2450,7 @@ __global__ __launch_bounds__(kThreads) void k_ht_partial(Geom g, Hyper hp, Plane
       }
     }
     // wave-reduce and accumulate (lane 0 holds the row's values)
-    acc[0] += (double)fh;  // identical on every lane
+    if (lane == 0) acc[0] += (double)fh;  // identical on every lane
     for (int c = 0; c < kHTCand; ++c) {
       float fb = 0.f;
       for (int o = 0; o < NO; ++o) {
@@ -2455,13 +2458,14 @@ __global__ __launch_bounds__(kThreads) void k_ht_partial(Geom g, Hyper hp, Plane
         if (shift) vv = vv - sbuf[o];
         fb += vv * vv;
       }
-      acc[1 + 3 * c] += (double)fb;
-      acc[2 + 3 * c] += (double)wave_sum(ip[c]);
-      acc[3 + 3 * c] += (double)wave_sum(nq[c]);
+      const float sip = wave_sum(ip[c]), snq = wave_sum(nq[c]);
+      if (lane == 0) {
+        acc[1 + 3 * c] += (double)fb;
+        acc[2 + 3 * c] += (double)sip;
+        acc[3 + 3 * c] += (double)snq;
+      }
     }
   }
-  if (lane == 0)
-    for (int i = 0; i < kHTSums; ++i) accs[w][i] = acc[i];
   __syncthreads();
   if (threadIdx.x < kHTSums) {
     const int i = threadIdx.x;

@@ -236,7 +236,11 @@ int stage_wy(AdmmCtx* c, hipStream_t s) {
   ProfScope ps(c, ADMM_PROF_SMALL, s);
   launch_wy_grad(g, c->hp, c->buf.gates[ADMM_H], c->buf.a, c->buf.dual_y, c->buf.wy, c->U, c->wy_slab,
                  c->wy_nsplit, s);
-  launch_wy_reduce(g, c->wy_slab, c->wy_nsplit, c->Gy, s);
+  if (!c->comm && !c->host_ar) {   // one process: reduce and apply in one launch
+    launch_wy_reduce(g, c->hp, c->wy_slab, c->wy_nsplit, c->Gy, c->buf.wy, s);
+    return ADMM_OK;
+  }
+  launch_wy_reduce(g, c->hp, c->wy_slab, c->wy_nsplit, c->Gy, nullptr, s);
   int rc = allreduce_f32(c, c->Gy, (size_t)g.H * g.O, s);
   if (rc) return rc;
   launch_wy_apply(g, c->hp, c->Gy, c->buf.wy, s);

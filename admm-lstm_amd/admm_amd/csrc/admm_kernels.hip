@@ -2336,7 +2336,21 @@ __global__ __launch_bounds__(kThreads) void k_wy_slab(Geom g, const float* Sh, c
   slab[blockIdx.y * nHO + i] = s;
 }
 
-__global__ __launch_bounds__(kThreads) void k_wy_reduce(int64_t nHO, const float* slab, int nsplit, float* Gy) {
+// wy <- (theta* wy - G_y) / (theta* + beta'): admm theta = 1, dead search (admm.py:262-277) ->
+// theta* = 1/2, beta' = beta_y; no_dual_y theta* = 0.005, beta' = 2 beta_y (admm.no_dual_y.py:231-249)
+__device__ __forceinline__ float wy_new(const Hyper& hp, float w, float G) {
+  if (hp.variant == 0) {
+    const float th = 0.5f;
+    return (th * w - G) / (th + hp.beta_y);
+  }
+  const float th = 0.005f;
+  return (th * w - G) / (th + 2.f * hp.beta_y);
+}
+
+// G_y = sum of the slabs; with wy non-null (one process: no all-reduce in between) the same
+// thread also applies the update, one launch instead of two
+__global__ __launch_bounds__(kThreads) void k_wy_reduce(int64_t nHO, const float* slab, int nsplit, float* Gy,
+                                                          Hyper hp, float* wy) {
   const int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x;
   if (i >= nHO) return;
   double s = 0.0;
@@ -2349,19 +2363,15 @@ __global__ __launch_bounds__(kThreads) void k_wy_reduce(int64_t nHO, const float
     for (int u = 0; u < 8; ++u) s += (double)v[u];
   }
   for (; sp < nsplit; ++sp) s += (double)slab[(int64_t)sp * nHO + i];
-  Gy[i] = (float)s;
+  const float G = (float)s;
+  Gy[i] = G;
+  if (wy) wy[i] = wy_new(hp, wy[i], G);
 }
 
 __global__ __launch_bounds__(kThreads) void k_wy_apply(int64_t nHO, Hyper hp, const float* Gy, float* wy) {
   const int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x;
   if (i >= nHO) return;
-  if (hp.variant == 0) {
-    const float th = 0.5f;  // theta = 1, dead search (admm.py:262-277) -> 1/2
-    wy[i] = (th * wy[i] - Gy[i]) / (th + hp.beta_y);
-  } else {
-    const float th = 0.005f;  // theta = 0.01 -> 0.005 (admm.no_dual_y.py:231-249)
-    wy[i] = (th * wy[i] - Gy[i]) / (th + 2.f * hp.beta_y);
-  }
+  wy[i] = wy_new(hp, wy[i], Gy[i]);
 }
 
 // ============================================================================ h_T
@@ -2909,9 +2919,10 @@ void launch_wy_grad(const Geom& g, const Hyper& hp, const float* Sh, const float
   k_wy_slab<<<grid, kThreads, 0, s>>>(g, Sh, U, slab, nsplit);
 }
 
-void launch_wy_reduce(const Geom& g, const float* slab, int nsplit, float* Gy, hipStream_t s) {
+void launch_wy_reduce(const Geom& g, const Hyper& hp, const float* slab, int nsplit, float* Gy, float* wy_apply,
+                      hipStream_t s) {
   const int64_t nHO = (int64_t)g.H * g.O;
-  k_wy_reduce<<<cdiv64(nHO, kThreads), kThreads, 0, s>>>(nHO, slab, nsplit, Gy);
+  k_wy_reduce<<<cdiv64(nHO, kThreads), kThreads, 0, s>>>(nHO, slab, nsplit, Gy, hp, wy_apply);
 }
 
 void launch_wy_apply(const Geom& g, const Hyper& hp, const float* Gy, float* wy, hipStream_t s) {

@@ -236,7 +236,9 @@ void launch_select(const Geom& g, const Hyper& hp, const SelectArgs& a, hipStrea
 int wy_splits(const Geom& g);
 void launch_wy_grad(const Geom& g, const Hyper& hp, const float* Sh, const float* a, const float* Ly,
                     const float* wy, float* U, float* slab, int nsplit, hipStream_t s);
-void launch_wy_reduce(const Geom& g, const float* slab, int nsplit, float* Gy, hipStream_t s);
+// wy_apply non-null: also wy <- update(wy, G_y) in the same launch (no all-reduce of G_y needed)
+void launch_wy_reduce(const Geom& g, const Hyper& hp, const float* slab, int nsplit, float* Gy, float* wy_apply,
+                      hipStream_t s);
 void launch_wy_apply(const Geom& g, const Hyper& hp, const float* Gy, float* wy, hipStream_t s);
 
 // ---- h_T search (admm.py:459-487; admm.no_dual_y.py:426-449), a update, duals at T

@@ -1033,6 +1033,15 @@ __global__ __launch_bounds__(kThreads) void k_reduce_g(int Kd, int H, Hyper hp, 
   const int64_t st = 4 * per_q;
   double s = 0.0;
   int sp = 0;
+  // 32 loads in flight while there are that many splits (the x side reduces the sweep's 256
+  // per-workgroup slabs with only 64 workgroups), then 8; the summation order is the same
+  for (; sp + 32 <= nsplit; sp += 32) {
+    float v[32];
+#pragma unroll
+    for (int u = 0; u < 32; ++u) v[u] = p[(int64_t)(sp + u) * st];
+#pragma unroll
+    for (int u = 0; u < 32; ++u) s += (double)v[u];
+  }
   for (; sp + 8 <= nsplit; sp += 8) {
     float v[8];
 #pragma unroll

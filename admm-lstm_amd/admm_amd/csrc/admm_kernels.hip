@@ -2364,6 +2364,13 @@ __global__ __launch_bounds__(kThreads) void k_wy_reduce(int64_t nHO, const float
   if (i >= nHO) return;
   double s = 0.0;
   int sp = 0;
+  for (; sp + 32 <= nsplit; sp += 32) {   // one workgroup at O = 1: 32 loads in flight, same order
+    float v[32];
+#pragma unroll
+    for (int u = 0; u < 32; ++u) v[u] = slab[(int64_t)(sp + u) * nHO + i];
+#pragma unroll
+    for (int u = 0; u < 32; ++u) s += (double)v[u];
+  }
   for (; sp + 8 <= nsplit; sp += 8) {   // loads issued 8 at a time, the same summation order
     float v[8];
 #pragma unroll

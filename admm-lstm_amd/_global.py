@@ -5,8 +5,11 @@ Frederick2309/ADMM-LSTM): ``device`` is fixed at import (``_global.py:217``);
 ``info``/``warning`` print a timestamped line and append it to a log file;
 ``error`` prints, logs and terminates with ``SystemExit(code)``
 (``_global.py:183-188``); ``log_assert`` calls ``error`` when its condition is
-false (``_global.py:197-200``).  The reference's colour helpers, GlobalDict,
-memory probes and decorators are not on the optimizer path and are not kept.
+false (``_global.py:197-200``).  ``global_dict`` is the process-wide key/value
+store ``demo.py`` imports (``demo.py:30, 286, 364``; reference ``_global.py:68-88``):
+the file logger registers itself there under ``'loggers'`` and publishes the path it
+writes to as ``'logger_filename'`` (``_global.py:113-142``).  The reference's colour
+helpers, memory probes and decorators are not on the optimizer path and are not kept.
 """
 from __future__ import annotations
 
@@ -15,27 +18,85 @@ import logging
 import os
 import sys
 from datetime import datetime
-from typing import Any, NoReturn
+from typing import Any, Dict, Iterator, NoReturn
 
 import torch
 
 device = torch.device('cuda' if torch.cuda.is_available() else 'cpu')
+PATH = os.path.abspath(os.getcwd())          # _global.py:92 (the run's working directory)
 
-_LOG_PATH = os.path.join('logs', 'ADMMRunningLogs.log')
-_logger: logging.Logger | None = None
+
+class GlobalDict:
+    """Process-wide key/value store (``_global.py:68-88``): ``set``/``get``/``keys`` and item
+    access; ``get`` of a missing key raises ``KeyError`` as the reference's does."""
+
+    def __init__(self) -> None:
+        self.contents: Dict[str, Any] = {}
+
+    def set(self, key: str, value: Any) -> None:
+        self.contents[key] = value
+
+    def get(self, key: str) -> Any:
+        return self.contents[key]
+
+    def keys(self):
+        return self.contents.keys()
+
+    def __setitem__(self, key: str, value: Any) -> None:
+        self.set(key, value)
+
+    def __getitem__(self, key: str) -> Any:
+        return self.get(key)
+
+    def __contains__(self, key: object) -> bool:
+        return key in self.contents
+
+    def __iter__(self) -> Iterator[str]:
+        return iter(self.contents)
+
+
+global_dict = GlobalDict()
+global_dict.set('loggers', {})
+
+_DEFAULT_LOG = os.path.join('logs', 'ADMMRunningLogs.log')
 _COLOURS = {'INFO': '\033[32m', 'WARNING': '\033[33m', 'ERROR': '\033[31m', 'ASSERTION FAILURE': '\033[31m'}
 
 
+def _free_name(path: str) -> str:
+    """``x.log`` if it does not exist yet, else the first free ``x_1.log``, ``x_2.log`` ...
+    (one log file per run, _global.py:121-131)."""
+    if not os.path.exists(path):
+        return path
+    stem = path[:-len('.log')] if path.endswith('.log') else path
+    i = 1
+    while os.path.exists(f'{stem}_{i}.log'):
+        i += 1
+    return f'{stem}_{i}.log'
+
+
+def _logger_for(filename: str | None = None) -> logging.Logger:
+    """The run's file logger, created on first use and registered in ``global_dict``."""
+    loggers: Dict[str, logging.Logger] = global_dict['loggers']
+    if filename is None:
+        if loggers:
+            filename = next(iter(loggers))
+        else:
+            os.makedirs(os.path.dirname(_DEFAULT_LOG), exist_ok=True)
+            filename = _DEFAULT_LOG
+    if filename not in loggers:
+        filename = _free_name(filename)
+        lg = logging.getLogger(filename)
+        lg.setLevel(logging.DEBUG)
+        handler = logging.FileHandler(filename)
+        handler.setFormatter(logging.Formatter('%(asctime)s - %(name)s - %(levelname)s - %(message)s'))
+        lg.addHandler(handler)
+        loggers[filename] = lg
+    global_dict.set('logger_filename', filename)
+    return loggers[filename]
+
+
 def _log(level: int, msg: str) -> None:
-    global _logger
-    if _logger is None:
-        os.makedirs(os.path.dirname(_LOG_PATH), exist_ok=True)
-        _logger = logging.getLogger('admm_amd')
-        _logger.setLevel(logging.DEBUG)
-        handler = logging.FileHandler(_LOG_PATH)
-        handler.setFormatter(logging.Formatter('%(asctime)s - %(levelname)s - %(message)s'))
-        _logger.addHandler(handler)
-    _logger.log(level, msg)
+    _logger_for().log(level, msg)
 
 
 def _emit(tag: str, msg: Any) -> None:

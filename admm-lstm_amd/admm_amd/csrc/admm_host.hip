@@ -77,6 +77,7 @@ int dalloc(T** p, size_t n) {
 }  // namespace
 
 constexpr int kMaxSweepStreams = 4;
+constexpr int kMaxOutputs = 4096;
 
 struct AdmmCtx {
   Geom g{};
@@ -425,7 +426,9 @@ int check_dims(const AdmmDims* d) {
     return fail(ADMM_EINVAL, "all dims must be positive (B=%lld T=%d D=%d H=%d O=%d)", (long long)d->batch,
                 d->seq_len, d->input_size, d->hidden_size, d->output_size);
   if (d->global_batch < d->batch) return fail(ADMM_EINVAL, "global_batch < batch");
-  if (d->output_size > 8) return fail(ADMM_EINVAL, "output_size %d > 8 is not supported", d->output_size);
+  // the h_T kernels keep one LDS row of O floats per wave (4 waves per workgroup)
+  if (d->output_size > kMaxOutputs)
+    return fail(ADMM_EINVAL, "output_size %d > %d is not supported", d->output_size, kMaxOutputs);
   if (d->batch * (int64_t)d->seq_len >= (1ll << 31))
     return fail(ADMM_EINVAL, "batch*seq_len = %lld rows per device exceeds 2^31-1", (long long)(d->batch * (int64_t)d->seq_len));
   return ADMM_OK;
@@ -464,6 +467,11 @@ int admm_create(const AdmmDims* dims, const AdmmParams* params, int device, Admm
   g.H = dims->hidden_size;
   g.O = dims->output_size;
   g.set_T();
+  // kernel-choice knobs live in the context's Geom (a per-context read: tests flip them
+  // between contexts of one process)
+  if (const char* e = std::getenv("ADMM_SWEEP_R16")) g.r16 = std::atoi(e) != 0;
+  if (const char* e = std::getenv("ADMM_TRIAL_MX")) g.trial_mx = std::atoi(e) != 0;
+  if (const char* e = std::getenv("ADMM_ATR_WIDE")) g.atr_wide = std::atoi(e) != 0;
   if (const char* e = std::getenv("ADMM_SWEEP_SPLIT"))
     c->sweep_split = std::max(1, std::min(kMaxSweepStreams, std::atoi(e)));
   c->sweep_rows = sweep_rows_ok(g);

@@ -2393,48 +2393,61 @@ __global__ __launch_bounds__(kThreads) void k_wy_apply(int64_t nHO, Hyper hp, co
 // ============================================================================ h_T
 // Per row: u = h wy - a - s,  g = gamma u wy^T (admm: gamma = rho_y via autograd; no_dual_y:
 // gamma = rho_h), candidates beta(theta) for theta = 0.1 * 2^c.
-constexpr int kMaxO = 8;
+// Output columns per pass of the generic (runtime O) h_T kernels: their per-candidate
+// accumulators stay in registers and any O is covered by ceil(O / kOChunk) passes over the row.
+constexpr int kOChunk = 8;
 
-template <int N>
-struct HTRowT {
-  float u[N];
+// u = h wy - a - s of one row: in registers for a compile-time O (the O = 1 hot path), else in
+// a per-wave LDS row of O floats (every lane writes the same value it holds after wave_sum)
+template <int OC>
+struct HTRow {
+  float reg[OC > 0 ? OC : 1];
+  float* lds;
+  __device__ __forceinline__ float get(int o) const {
+    if constexpr (OC > 0) return reg[o];
+    else return lds[o];
+  }
+  __device__ __forceinline__ void set(int o, float v) {
+    if constexpr (OC > 0) reg[o] = v;
+    else lds[o] = v;
+  }
 };
-// array width for a compile-time output count (O = 1: registers), else the runtime bound kMaxO
-#define HT_W (OC > 0 ? OC : kMaxO)
 
 template <int OC>
-__device__ __forceinline__ void ht_row_u(const Geom& g, const float* h, const float* a_row, const float* s_row,
-                                         const float* wy, HTRowT<HT_W>& r) {
-  const int NO = OC > 0 ? OC : g.O;   // output width: compile-time for O = 1 (arrays stay in registers)
+__device__ __forceinline__ void ht_row_u(const Geom& g, const float* h, const float* a_row, const float* ly_row,
+                                         float ry, const float* wy, HTRow<OC>& r) {
+  const int NO = OC > 0 ? OC : g.O;
   const int lane = threadIdx.x & 63;
   for (int o = 0; o < NO; ++o) {
     float s = 0.f;
     for (int j = lane; j < g.H; j += kWave) s += h[j] * wy[(int64_t)j * NO + o];
     s = wave_sum(s);
     float u = s - a_row[o];
-    if (s_row) u = u - s_row[o];
-    r.u[o] = u;
+    if (ly_row) u = u - ly_row[o] / ry;
+    r.set(o, u);
   }
 }
 
 template <int OC>
-__device__ __forceinline__ float ht_grad(const Geom& g, const Hyper& hp, const HTRowT<HT_W>& r, const float* wy, int j) {
-  const int NO = OC > 0 ? OC : g.O;   // output width: compile-time for O = 1 (arrays stay in registers)
+__device__ __forceinline__ float ht_grad(const Geom& g, const Hyper& hp, const HTRow<OC>& r, const float* wy, int j) {
+  const int NO = OC > 0 ? OC : g.O;
   float s = 0.f;
   if (hp.variant == 0) {
     const float ry = hp.rho[6];
-    for (int o = 0; o < NO; ++o) s += (ry * r.u[o]) * wy[(int64_t)j * NO + o];
+    for (int o = 0; o < NO; ++o) s += (ry * r.get(o)) * wy[(int64_t)j * NO + o];
     return s;
   }
-  for (int o = 0; o < NO; ++o) s += r.u[o] * wy[(int64_t)j * NO + o];
+  for (int o = 0; o < NO; ++o) s += r.get(o) * wy[(int64_t)j * NO + o];
   return hp.rho[5] * s;
 }
 
+// OC > 0: compile-time output count; OC == 0: runtime g.O, 4 * g.O floats of dynamic LDS
 template <int OC>
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(8))) void k_ht_partial(Geom g, Hyper hp, Planes6 S, Planes6 L, const float* a,
                                                            const float* Ly, const float* wy, double* part) {
-  const int NO = OC > 0 ? OC : g.O;   // output width: compile-time for O = 1 (arrays stay in registers)
-  __shared__ double red[4];
+  constexpr int CW = OC > 0 ? OC : kOChunk;
+  const int NO = OC > 0 ? OC : g.O;
+  extern __shared__ float ht_u[];
   __shared__ double accs[4][kHTSums];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const float ry = hp.rho[6], rh = hp.rho[5];
@@ -2446,47 +2459,51 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(8))) v
   double* acc = accs[w];
   if (lane == 0)
     for (int i = 0; i < kHTSums; ++i) acc[i] = 0.0;
-  float sbuf[HT_W];
   for (int64_t b = (int64_t)blockIdx.x * 4 + w; b < g.B; b += (int64_t)gridDim.x * 4) {
     const float* h = S.p[5] + b * rs + tofs;
     const float* o_ = S.p[3] + b * rs + tofs;
     const float* c_ = S.p[4] + b * rs + tofs;
     const float* lh = L.p[5] + b * rs + tofs;
-    if (shift)
-      for (int o = 0; o < NO; ++o) sbuf[o] = Ly[b * NO + o] / ry;
-    HTRowT<HT_W> r;
-    ht_row_u<OC>(g, h, a + b * NO, shift ? sbuf : nullptr, wy, r);
+    const float* ly = shift ? Ly + b * NO : nullptr;
+    HTRow<OC> r;
+    r.lds = ht_u + w * NO;
+    ht_row_u<OC>(g, h, a + b * NO, ly, ry, wy, r);
     float fh = 0.f;
-    for (int o = 0; o < NO; ++o) fh += r.u[o] * r.u[o];
-    float v[kHTCand][HT_W], ip[kHTCand], nq[kHTCand];
-    for (int c = 0; c < kHTCand; ++c) {
-      ip[c] = 0.f; nq[c] = 0.f;
-      for (int o = 0; o < NO; ++o) v[c][o] = 0.f;
-    }
-    for (int j = lane; j < g.H; j += kWave) {
-      const float gj = ht_grad<OC>(g, hp, r, wy, j);
-      const float hj = h[j], pj = rh * o_[j] * tanhf(c_[j]) - lh[j];
-      for (int c = 0; c < kHTCand; ++c) {
-        const float th = ldexpf(0.1f, c);
-        const float bj = nd ? gj / th : (th * hj + pj - gj) / (th + rh);
-        const float dj = bj - hj;
-        ip[c] += gj * dj;
-        nq[c] += dj * dj;
-        for (int o = 0; o < NO; ++o) v[c][o] += bj * wy[(int64_t)j * NO + o];
+    for (int o = 0; o < NO; ++o) fh += r.get(o) * r.get(o);
+    float ip[kHTCand], nq[kHTCand], fb[kHTCand];
+    for (int c = 0; c < kHTCand; ++c) ip[c] = nq[c] = fb[c] = 0.f;
+    for (int o0 = 0; o0 < NO; o0 += CW) {
+      const int nw = NO - o0 < CW ? NO - o0 : CW;
+      float v[kHTCand][CW];
+      for (int c = 0; c < kHTCand; ++c)
+        for (int oo = 0; oo < CW; ++oo) v[c][oo] = 0.f;
+      for (int j = lane; j < g.H; j += kWave) {
+        const float gj = ht_grad<OC>(g, hp, r, wy, j);
+        const float hj = h[j], pj = rh * o_[j] * tanhf(c_[j]) - lh[j];
+        for (int c = 0; c < kHTCand; ++c) {
+          const float th = ldexpf(0.1f, c);
+          const float bj = nd ? gj / th : (th * hj + pj - gj) / (th + rh);
+          const float dj = bj - hj;
+          if (o0 == 0) {
+            ip[c] += gj * dj;
+            nq[c] += dj * dj;
+          }
+          for (int oo = 0; oo < nw; ++oo) v[c][oo] += bj * wy[(int64_t)j * NO + o0 + oo];
+        }
       }
+      for (int c = 0; c < kHTCand; ++c)
+        for (int oo = 0; oo < nw; ++oo) {
+          float vv = wave_sum(v[c][oo]) - a[b * NO + o0 + oo];
+          if (shift) vv = vv - ly[o0 + oo] / ry;
+          fb[c] += vv * vv;
+        }
     }
     // wave-reduce and accumulate (lane 0 holds the row's values)
     if (lane == 0) acc[0] += (double)fh;  // identical on every lane
     for (int c = 0; c < kHTCand; ++c) {
-      float fb = 0.f;
-      for (int o = 0; o < NO; ++o) {
-        float vv = wave_sum(v[c][o]) - a[b * NO + o];
-        if (shift) vv = vv - sbuf[o];
-        fb += vv * vv;
-      }
       const float sip = wave_sum(ip[c]), snq = wave_sum(nq[c]);
       if (lane == 0) {
-        acc[1 + 3 * c] += (double)fb;
+        acc[1 + 3 * c] += (double)fb[c];
         acc[2 + 3 * c] += (double)sip;
         acc[3 + 3 * c] += (double)snq;
       }
@@ -2497,7 +2514,6 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(8))) v
     const int i = threadIdx.x;
     part[(int64_t)blockIdx.x * kHTSums + i] = (accs[0][i] + accs[1][i]) + (accs[2][i] + accs[3][i]);
   }
-  (void)red;
 }
 
 // all kHTSums sums in one pass over the partials (per sum: thread t adds partials t, t + 256, ...,
@@ -2539,12 +2555,14 @@ __device__ __forceinline__ float ht_theta_star(const Hyper& hp, const double* su
 }
 
 // h_T update with theta* (admm.py:482-487), a update (489-502), dual h at T (532-539),
-// dual y (541-546, admm variant with with_dual_y).
+// dual y (541-546, admm variant with with_dual_y).  OC as k_ht_partial.
 template <int OC>
 __global__ __launch_bounds__(kThreads) void k_ht_apply(Geom g, Hyper hp, Planes6 S, Planes6 L, float* a, float* Ly,
                                                          const float* y, const float* wy, const double* sums,
                                                          DevStats* stats, int* status) {
-  const int NO = OC > 0 ? OC : g.O;   // output width: compile-time for O = 1 (arrays stay in registers)
+  constexpr int CW = OC > 0 ? OC : kOChunk;
+  const int NO = OC > 0 ? OC : g.O;
+  extern __shared__ float ht_u[];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const float ry = hp.rho[6], rh = hp.rho[5];
   const bool nd = hp.variant == 1;
@@ -2561,39 +2579,46 @@ __global__ __launch_bounds__(kThreads) void k_ht_apply(Geom g, Hyper hp, Planes6
   }
   const int64_t rs = (int64_t)g.TP() * g.H, tofs = (int64_t)g.T * g.H;
   const float Bry = (float)g.Bg * ry;
-  float sbuf[HT_W];
   for (int64_t b = (int64_t)blockIdx.x * 4 + w; b < g.B; b += (int64_t)gridDim.x * 4) {
     float* h = S.p[5] + b * rs + tofs;
     const float* o_ = S.p[3] + b * rs + tofs;
     const float* c_ = S.p[4] + b * rs + tofs;
     float* lh = L.p[5] + b * rs + tofs;
-    if (shift)
-      for (int o = 0; o < NO; ++o) sbuf[o] = Ly[b * NO + o] / ry;
-    HTRowT<HT_W> r;
-    ht_row_u<OC>(g, h, a + b * NO, shift ? sbuf : nullptr, wy, r);
-    float hw[HT_W];
-    for (int o = 0; o < NO; ++o) hw[o] = 0.f;
-    for (int j = lane; j < g.H; j += kWave) {
-      const float gj = ht_grad<OC>(g, hp, r, wy, j);
-      const float tc = tanhf(c_[j]);
-      const float hn = (th * h[j] + rh * o_[j] * tc - lh[j] - gj) / (th + rh);
-      h[j] = hn;
-      lh[j] = lh[j] + rh * (hn - o_[j] * tc);
-      for (int o = 0; o < NO; ++o) hw[o] += hn * wy[(int64_t)j * NO + o];
-    }
-    for (int o = 0; o < NO; ++o) {
-      const float hwo = wave_sum(hw[o]);
-      if (lane == 0) {
-        const int64_t i = b * NO + o;
-        float an;
-        if (!nd) {
-          const float corr = shift ? (float)g.Bg * Ly[i] : 0.f;
-          an = (2.f * y[i] + Bry * hwo - corr) / (2.f + Bry);
+    HTRow<OC> r;
+    r.lds = ht_u + w * NO;
+    ht_row_u<OC>(g, h, a + b * NO, shift ? Ly + b * NO : nullptr, ry, wy, r);
+    // the first pass writes the new h_T (and its dual); later passes re-read the lane's own h_T
+    for (int o0 = 0; o0 < NO; o0 += CW) {
+      const int nw = NO - o0 < CW ? NO - o0 : CW;
+      float hw[CW];
+      for (int oo = 0; oo < CW; ++oo) hw[oo] = 0.f;
+      for (int j = lane; j < g.H; j += kWave) {
+        float hn;
+        if (o0 == 0) {
+          const float gj = ht_grad<OC>(g, hp, r, wy, j);
+          const float tc = tanhf(c_[j]);
+          hn = (th * h[j] + rh * o_[j] * tc - lh[j] - gj) / (th + rh);
+          h[j] = hn;
+          lh[j] = lh[j] + rh * (hn - o_[j] * tc);
         } else {
-          an = (Bry * hwo + 2.f * y[i]) / (2.f + Bry);
+          hn = h[j];
         }
-        a[i] = an;
-        if (shift) Ly[i] = Ly[i] + ry * (an - hwo);
+        for (int oo = 0; oo < nw; ++oo) hw[oo] += hn * wy[(int64_t)j * NO + o0 + oo];
+      }
+      for (int oo = 0; oo < nw; ++oo) {
+        const float hwo = wave_sum(hw[oo]);
+        if (lane == 0) {
+          const int64_t i = b * NO + o0 + oo;
+          float an;
+          if (!nd) {
+            const float corr = shift ? (float)g.Bg * Ly[i] : 0.f;
+            an = (2.f * y[i] + Bry * hwo - corr) / (2.f + Bry);
+          } else {
+            an = (Bry * hwo + 2.f * y[i]) / (2.f + Bry);
+          }
+          a[i] = an;
+          if (shift) Ly[i] = Ly[i] + ry * (an - hwo);
+        }
       }
     }
   }
@@ -2637,14 +2662,7 @@ void launch_sweep_t(const Geom& g, int t, const Weights& w, const Hyper& hp, con
 }
 
 // 16-row tiles for 256 < H <= 512 (ADMM_SWEEP_R16=0: those shapes take the per-t sweep)
-static bool sweep_r16(const Geom& g) {
-  static int on = -1;
-  if (on < 0) {
-    const char* e = std::getenv("ADMM_SWEEP_R16");
-    on = e ? std::atoi(e) != 0 : 1;
-  }
-  return on && g.H > 256 && g.H <= 512 && g.H % 64 == 0;
-}
+static bool sweep_r16(const Geom& g) { return g.r16 && g.H > 256 && g.H <= 512 && g.H % 64 == 0; }
 
 bool sweep_rows_ok(const Geom& g) {
   // 32-bit buffer offsets: a [B][T+1][H] plane and a [B*T][H] z-cache plane in bytes
@@ -2729,14 +2747,7 @@ void launch_resid(const Geom& g, const Hyper& hp, const ResidArgs& a, hipStream_
   k_resid<<<grid, kThreads, 0, s>>>(g, hp, a);
 }
 
-static int g_atr_wide = -1;
-bool atr_wide(const Geom& g) {
-  if (g_atr_wide < 0) {
-    const char* e = std::getenv("ADMM_ATR_WIDE");
-    g_atr_wide = e ? std::atoi(e) : 1;
-  }
-  return g_atr_wide && g.H % 256 == 0;
-}
+bool atr_wide(const Geom& g) { return g.atr_wide && g.H % 256 == 0; }
 
 int atr_splits(const Geom& g, int side) {
   const int Kd = side == 0 ? g.D : g.H;
@@ -2860,14 +2871,9 @@ void launch_apply_fix(const Geom& g, const float* x, const float* dW, const floa
 
 bool trial_rows_ok(const Geom& g) { return g.H % 256 == 0; }
 
-static int g_trial_mx = -1;
 bool trial_mx_ok(const Geom& g) {   // ADMM_TRIAL_MX=0: the x side on k_trial_rows (VALU q)
-  if (g_trial_mx < 0) {
-    const char* e = std::getenv("ADMM_TRIAL_MX");
-    g_trial_mx = e ? std::atoi(e) != 0 : 1;
-  }
   // 32-bit buffer offsets within one gate plane
-  return g_trial_mx && g.H % 256 == 0 && g.D <= 16 && g.BT() * g.H * 4 < (int64_t)INT32_MAX;
+  return g.trial_mx && g.H % 256 == 0 && g.D <= 16 && g.BT() * g.H * 4 < (int64_t)INT32_MAX;
 }
 
 void launch_trial_fast(const Geom& g, int side, int pass, const float* zc, const float* tgt, const float* Q,
@@ -2954,7 +2960,7 @@ int ht_blocks(const Geom& g) {   // one row per wave up to B = 8192 (each row is
 void launch_ht_partial(const Geom& g, const Hyper& hp, const Planes6& S, const Planes6& L, const float* a,
                        const float* Ly, const float* wy, double* part, int nblk, hipStream_t s) {
   if (g.O == 1) k_ht_partial<1><<<nblk, kThreads, 0, s>>>(g, hp, S, L, a, Ly, wy, part);
-  else k_ht_partial<0><<<nblk, kThreads, 0, s>>>(g, hp, S, L, a, Ly, wy, part);
+  else k_ht_partial<0><<<nblk, kThreads, 4 * g.O * sizeof(float), s>>>(g, hp, S, L, a, Ly, wy, part);
 }
 
 void launch_ht_reduce(const double* part, int nblk, double* sums, hipStream_t s) {
@@ -2964,7 +2970,7 @@ void launch_ht_reduce(const double* part, int nblk, double* sums, hipStream_t s)
 void launch_ht_apply(const Geom& g, const Hyper& hp, const Planes6& S, const Planes6& L, float* a, float* Ly,
                      const float* y, const float* wy, const double* sums, DevStats* stats, int* status, hipStream_t s) {
   if (g.O == 1) k_ht_apply<1><<<ht_blocks(g), kThreads, 0, s>>>(g, hp, S, L, a, Ly, y, wy, sums, stats, status);
-  else k_ht_apply<0><<<ht_blocks(g), kThreads, 0, s>>>(g, hp, S, L, a, Ly, y, wy, sums, stats, status);
+  else k_ht_apply<0><<<ht_blocks(g), kThreads, 4 * g.O * sizeof(float), s>>>(g, hp, S, L, a, Ly, y, wy, sums, stats, status);
 }
 
 }  // namespace admm

@@ -38,6 +38,9 @@ struct Geom {
   int64_t Bg;   // global rows (a-update constant)
   int T, D, H, O;
   DivU32 dT{};  // by T; set with set_T() (B*T < 2^31 is checked at create)
+  // kernel-choice knobs, read from the environment once per context (admm_create):
+  // ADMM_SWEEP_R16, ADMM_TRIAL_MX, ADMM_ATR_WIDE
+  bool r16 = true, trial_mx = true, atr_wide = true;
   __host__ __device__ int64_t BT() const { return B * (int64_t)T; }
   __host__ __device__ int TP() const { return T + 1; }
   void set_T() { dT = DivU32::make((uint32_t)T); }

@@ -178,14 +178,23 @@ class AdmmOptimizerBase(object):
             raise RuntimeError('distributed=True needs an initialised torch.distributed process group')
         self._world, self._rank = dist.get_world_size(), dist.get_rank()
         n = torch.tensor([self.batch_size], dtype=torch.int64)
-        if dist.get_backend() == 'nccl':
+        if self._rccl_group():
             n = n.to(self._device)
         dist.all_reduce(n)
         self._global_batch = int(n.item())
 
+    @staticmethod
+    def _rccl_group() -> bool:
+        """True when the default group reaches the GPU through RCCL: backend 'nccl', or a
+        combined per-device backend string such as 'cpu:gloo,cuda:nccl'."""
+        import torch.distributed as dist
+        return 'nccl' in str(dist.get_backend()).lower()
+
     def _connect_comm(self) -> None:
         import torch.distributed as dist
-        if dist.get_backend() != 'nccl':
+        if not self._rccl_group():
+            warning(f'process group backend {dist.get_backend()!r} has no RCCL: every all-reduce of step() '
+                    'is staged through host memory (slow; meant for tests)', use_logger=False)
             self._connect_host_comm()
             return
         uid = ctypes.create_string_buffer(N.NCCL_UNIQUE_ID_BYTES)
@@ -211,7 +220,8 @@ class AdmmOptimizerBase(object):
                 t = torch.from_numpy(arr)   # shares the library's staging buffer
                 dist.all_reduce(t)
                 return 0
-            except Exception:  # pragma: no cover - reported by the library as ADMM_ECOMM
+            except Exception as exc:  # pragma: no cover - re-raised by step() after the library fails
+                self._host_ar_error = exc
                 return 1
 
         self._host_ar = N.HOST_ALLREDUCE_FN(allreduce)   # keep the thunk alive with the context
@@ -282,7 +292,12 @@ class AdmmOptimizerBase(object):
             N.check(self._lib.admm_set_with_dual_y(self._ctx, int(flag)), 'admm_set_with_dual_y')
             self._dual_y_sent = flag
         self._sync_bindings()
-        N.check(self._lib.admm_step(self._ctx, N.stream_handle(self._device)), 'admm_step')
+        self._host_ar_error = None
+        rc = self._lib.admm_step(self._ctx, N.stream_handle(self._device))
+        if rc != 0 and self._host_ar_error is not None:   # the host-staged all-reduce's own error
+            raise N.AdmmError(f'admm_step failed (code {rc}): the host-staged all-reduce raised '
+                              f'{self._host_ar_error!r}') from self._host_ar_error
+        N.check(rc, 'admm_step')
         self._snapshot()
         self._poll_status()
 

@@ -75,8 +75,27 @@ def tgt_from_sweep(H: int) -> bool:
     return persistent_sweep(H) and os.environ.get('ADMM_TGT_SWEEP', '1') != '0'
 
 
+def survey_terms(B: int, T: int, D: int, H: int):
+    """SURVEY.md 8(d)'s algorithmic work per step: (F_w, B_w) of the eight weight updates and
+    (F_B, B_B) of the time sweep.  B_B = 4 B T (D + 25 H): per (b, t) read x_t, h_{t-1},
+    c_{t-1}, 6 gates and 6 duals, write 6 gates and 5 duals."""
+    F_w = T * 4.0 * (3 * 2.0 * B * H * H + 4 * 2.0 * B * D * H)
+    B_w = 64.0 * B * T * (D + 3 * H)
+    F_B = T * 2.0 * B * (D + H) * 4 * H
+    B_B = 4.0 * B * T * (D + 25 * H)
+    return (F_w, B_w), (F_B, B_B)
+
+
+def step_roofline_s(B: int, T: int, D: int, H: int) -> float:
+    """t_roof = sum over the two phases of max(F / fp32 MFMA peak, B / HBM peak) (SURVEY.md 8(d);
+    3.77 ms at C3)."""
+    return sum(max(f / PEAK_FP32_MFMA, b / PEAK_HBM) for f, b in survey_terms(B, T, D, H))
+
+
 def roofline_terms(cls: str, B: int, T: int, D: int, H: int):
-    """Algorithmic (flops, bytes) of ONE launch of a kernel class."""
+    """(flops, bytes) of ONE launch of a kernel class as this design moves them:
+    for the sweep these include the z-cache, target and G_x-partial writes that replace work
+    of the next step's x stage (bench reports SURVEY.md 8(d)'s algorithmic bytes beside them)."""
     f4 = 4  # bytes per fp32
     tgt = tgt_from_sweep(H)
     if cls == 'sweep':            # whole sweep t = 1..T: per t [B, D+H] x [D+H, 4H] + fused gate/dual updates
@@ -143,33 +162,76 @@ def pmc_traffic(cls: str, cfg_name: str):
     return per
 
 
-def cpu_baseline(cfg_name: str, seconds_hint: float = 20.0):
-    """Time the CPU oracle (reference op structure) on a bounded sample of the workload."""
+def host_cpu():
+    """(model name, sockets, physical cores per socket) of this host from /proc/cpuinfo."""
+    model, phys = 'unknown', {}
+    try:
+        cur = {}
+        for line in open('/proc/cpuinfo').read().splitlines() + ['']:
+            if not line.strip():
+                if 'physical id' in cur and 'core id' in cur:
+                    phys.setdefault(cur['physical id'], set()).add(cur['core id'])
+                cur = {}
+                continue
+            k, _, v = line.partition(':')
+            cur[k.strip()] = v.strip()
+            if k.strip() == 'model name':
+                model = v.strip()
+    except OSError:  # pragma: no cover
+        pass
+    sockets = len(phys) or 1
+    cores = max((len(v) for v in phys.values()), default=os.cpu_count() or 1)
+    return model, sockets, cores
+
+
+def cpu_baseline(cfg_name: str, timed_steps: int = 3, crosscheck_threads: int = 8):
+    """SURVEY.md 8(d) CPU-baseline protocol on this host: the CPU oracle (a port of the reference's
+    op structure, oracle/admm_oracle.py) on the FULL batch of the config, step 1 untimed (it is
+    cheaper: zero x-side gradients), the median of steps 2..1+timed_steps on min(16, physical
+    cores per socket) threads -- the GPU's CPU share on the box -- and one more step on
+    ``crosscheck_threads`` threads to compare with the survey container's 8-thread 27.6 s/it at C3."""
     from oracle import admm_oracle as O
     from parameters import example_parameter_dictionary
     B, T, D, H, variant, gen = CONFIGS[cfg_name]
+    model, sockets, per_socket = host_cpu()
     try:
-        cores = len(os.sched_getaffinity(0))
+        avail = len(os.sched_getaffinity(0))
     except AttributeError:  # pragma: no cover
-        cores = os.cpu_count() or 1
-    threads = max(1, min(cores, 16))
+        avail = os.cpu_count() or 1
+    threads = max(1, min(16, per_socket, avail))
     torch.set_num_threads(threads)
-    frac = 4 if B >= 4096 else 1
-    Bs = B // frac
-    x, y = make_data(gen, Bs, T, D)
+    x, y = make_data(gen, B, T, D)
     torch.manual_seed(0)
     W = O.init_weights(D, H, 1)
     st = O.init_state(x, y, W)
     stp = O.Stepper(O.Hyper.from_dict(example_parameter_dictionary['GoogleStock'], variant))
-    stp.step(st)                      # step 1 is cheap (zero gradients); time step 2
-    t0 = time.time()
-    stp.step(st)
-    dt = time.time() - t0
+    times = []
+    for s in range(1 + timed_steps):
+        t0 = time.time()
+        stp.step(st)
+        times.append(time.time() - t0)
+        print(f'cpu_baseline: step {s + 1} on {threads} threads: {times[-1]:.2f} s', file=sys.stderr, flush=True)
+    med = sorted(times[1:])[len(times[1:]) // 2]
+    cross = None
+    if crosscheck_threads and crosscheck_threads != threads:
+        torch.set_num_threads(crosscheck_threads)
+        t0 = time.time()
+        stp.step(st)
+        cross = time.time() - t0
+        print(f'cpu_baseline: step {2 + timed_steps} on {crosscheck_threads} threads: {cross:.2f} s',
+              file=sys.stderr, flush=True)
+        torch.set_num_threads(threads)
     return {
-        'value': round(1.0 / (dt * frac), 6), 'unit': 'it/s', 'cores': threads, 'kind': 'port',
-        'sample': f'oracle/admm_oracle.py (reference op structure, fp32 torch CPU, {threads} threads): '
-                  f'{cfg_name} shapes T={T} D={D} H={H} at B={Bs} (1/{frac} batch), step 2 timed '
-                  f'({dt:.2f} s), scaled x1/{frac} to B={B}',
+        'value': round(1.0 / med, 6), 'unit': 'it/s', 'cores': threads, 'kind': 'port',
+        'sample': f'oracle/admm_oracle.py (reference op structure, fp32 torch CPU) on the full {cfg_name} batch '
+                  f'B={B} T={T} D={D} H={H}: median of steps 2-{1 + timed_steps} = {med:.2f} s/it '
+                  f'(steps: {", ".join(f"{t:.2f}" for t in times)} s) on {threads} threads; '
+                  + (f'step {2 + timed_steps} on {crosscheck_threads} threads {cross:.2f} s '
+                     f'(survey container, 8 threads, reference itself: 27.6 s/it at C3); ' if cross else '')
+                  + f'host: {model}, {sockets} socket(s) x {per_socket} physical cores, {avail} CPUs visible',
+        'median_step_s': round(med, 3), 'step_s': [round(t, 3) for t in times],
+        'crosscheck': {'threads': crosscheck_threads, 'step_s': round(cross, 3)} if cross else None,
+        'host_cpu': {'model': model, 'sockets': sockets, 'physical_cores_per_socket': per_socket, 'visible_cpus': avail},
     }
 
 
@@ -181,6 +243,7 @@ def main():
     ap.add_argument('--config', default='c3', choices=sorted(CONFIGS))
     ap.add_argument('--scaling', default='weak', choices=['weak', 'strong'])
     ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--cpu-steps', type=int, default=3, help='timed CPU-baseline steps after step 1 (median)')
     ap.add_argument('--profile-classes', default='sweep,trial,trial_h,trial_extra,atr_x,atr_h,qgemm_x,qgemm_h,resid,small')
     args = ap.parse_args()
 
@@ -273,6 +336,9 @@ def main():
         n = prof[cls][1]
         avg_s = ms / n / 1e3
         flops, nbytes = roofline_terms(cls, per, T, D, H)
+        design_bytes = nbytes
+        if cls == 'sweep':          # the sweep's algorithmic work is (F_B, B_B)
+            flops, nbytes = survey_terms(per, T, D, H)[1]
         peak_mfma = PEAK_SPLIT3_MFMA if cls in SPLIT3_CLASSES else PEAK_FP32_MFMA
         t_mfma, t_hbm = flops / peak_mfma, nbytes / PEAK_HBM
         if t_mfma >= t_hbm:
@@ -282,20 +348,26 @@ def main():
             roof = {'bound': 'hbm', 'achieved': nbytes / avg_s / 1e9, 'peak': PEAK_HBM / 1e9, 'unit': 'GB/s'}
         roof['frac'] = roof['achieved'] / roof['peak']
         # traffic: measured HBM bytes per launch (PMC, DESIGN.md "Measurement"), next to the
-        # algorithmic bytes per launch it should match
+        # algorithmic bytes per launch and the bytes this design moves
         roof['traffic'] = pmc_traffic(cls, args.config)
         roof['algorithmic_bytes'] = nbytes
+        roof['design_bytes'] = design_bytes
+        roof['algorithmic_flops'] = flops
+        roof['mfma_frac_fp32'] = flops / avg_s / PEAK_FP32_MFMA    # SURVEY.md 8(d)'s MFMA fraction
         roof['kernel'] = cls
         roof['avg_launch_us'] = avg_s * 1e6
         roof['launches'] = n
         roof = {k: (round(v, 4) if isinstance(v, float) else v) for k, v in roof.items()}
+    t_roof = step_roofline_s(per, T, D, H)
+    step_roof = {'t_roof_ms': round(t_roof * 1e3, 4), 'step_frac': round(t_roof / (elapsed / args.steps), 4),
+                 'basis': 'SURVEY.md 8(d): sum over weight phase and sweep of max(F/157.3 TFLOP/s, B/8 TB/s)'}
     kernel_ms = {c: {'ms_per_step': round(ms / args.steps, 4), 'launches_per_step': n / args.steps}
                  for c, (ms, n) in sorted(prof.items(), key=lambda kv: -kv[1][0])}
 
     if rank == 0:
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
-            cpu = cpu_baseline(args.config)
+            cpu = cpu_baseline(args.config, args.cpu_steps)
         out = {
             'metric': 'ADMM iters/sec at hidden=256, batch=8192, seq=32; 1/2/4/8-GPU scaling',
             'value': round(value, 4), 'unit': 'it/s', 'n_gpus': world, 'steps': args.steps, 'warmup': args.warmup,
@@ -308,6 +380,7 @@ def main():
                        'output_size': 1, 'params': 'GoogleStock', 'parallelism': f'dp{world}',
                        'global_it_per_s': round(it_s, 4)},
             'roofline': roof,
+            'step_roofline': step_roof,
             'cpu_baseline': cpu,
             'kernels': kernel_ms,
             'line_search_k': list(stats['k'].values()),

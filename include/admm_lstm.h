@@ -122,9 +122,12 @@ int admm_step(AdmmCtx* ctx, void* stream);
    255, 461, 498); the drop-in forwards its current value before each admm_step. */
 int admm_set_with_dual_y(AdmmCtx* ctx, int32_t flag);
 
-/* The z cache (x_t Wx + h_{t-1} Wh for every t, produced by the time sweep) is reused by
-   the next step's first weight stage.  Call after modifying weights/gates/x outside
-   admm_step; the next step then recomputes it. */
+/* The library keeps caches derived from the bound state between steps: the z cache
+   (x_t Wx + h_{t-1} Wh for every t, produced by the time sweep), the next x stage's targets
+   tgt = dual/rho + gate and its X^T R partials (also left by the sweep), and the flag that the
+   h dual is zero before T (which lets the sweep skip loading it).  Call this after ANY write
+   outside admm_step to the weights, x, a gate plane or a dual plane (in particular the h dual
+   at t < T, which would otherwise be read as zero); the next step then rebuilds them. */
 int admm_invalidate_cache(AdmmCtx* ctx);
 
 /* Multi-GPU (one process per GPU): rank 0 calls admm_comm_unique_id, the bytes are

@@ -66,6 +66,10 @@ class Hyper:
         rho = {k: f32(pdict['rho'][k]) for k in ('i', 'f', 'g', 'o', 'c', 'h', 'y')}
         return Hyper(rho, beta, variant, with_dual_y)
 
+    def cast(self, dtype: torch.dtype) -> 'Hyper':
+        c = lambda d: {k: v.to(dtype) for k, v in d.items()}  # noqa: E731
+        return Hyper(c(self.rho), c(self.beta), self.variant, self.with_dual_y)
+
 
 @dataclass
 class State:
@@ -108,7 +112,7 @@ def lstm_gates(x: torch.Tensor, W: Dict[str, torch.Tensor]) -> Dict[str, torch.T
     """Initial primal state = LSTM forward (``blocks/lstm.py:65-88``)."""
     B, T, _ = x.shape
     H = W['h2i'].shape[0]
-    out = {q: torch.zeros(B, T + 1, H, dtype=x.dtype) for q in GATES6}
+    out = {q: torch.zeros(B, T + 1, H, dtype=x.dtype, device=x.device) for q in GATES6}
     for t in range(1, T + 1):
         xt, hp = x[:, t - 1, :], out['h'][:, t - 1, :]
         out['i'][:, t, :] = torch.sigmoid(xt @ W['x2i'] + hp @ W['h2i'])
@@ -136,18 +140,25 @@ def init_state(x, y, W, global_batch: Optional[int] = None) -> State:
     B, T, _ = x.shape
     H = W['h2i'].shape[0]
     S = lstm_gates(x, W)
-    L = {q: torch.zeros(B, T + 1, H) for q in GATES6}
-    L['y'] = torch.zeros(B, y.shape[1])
+    L = {q: torch.zeros(B, T + 1, H, dtype=x.dtype, device=x.device) for q in GATES6}
+    L['y'] = torch.zeros(B, y.shape[1], dtype=x.dtype, device=x.device)
     return State(x, y, {k: v.clone() for k, v in W.items()}, S, L, global_batch or B)
 
 
 # ----------------------------------------------------------------------------- helpers
 
 def _autograd(fn: Callable[[torch.Tensor], torch.Tensor], at: torch.Tensor) -> torch.Tensor:
-    """Gradient of a scalar objective by autograd (``admm.py:15-19``)."""
-    v = at.clone().detach().to(torch.float).requires_grad_(True)
+    """Gradient of a scalar objective by autograd (``admm.py:15-19``).  The reference casts to
+    fp32; an fp64 state (the arbitration oracle of the GPU tests) stays fp64."""
+    v = at.clone().detach().to(_wide(at)).requires_grad_(True)
     fn(v).backward()
     return v.grad
+
+
+def _wide(t: torch.Tensor) -> torch.dtype:
+    """The reference's hard-coded ``dtype=torch.float`` (admm.py:16, 302, 316), widened to fp64
+    when the state is fp64 -- identical for the reference's own fp32 state."""
+    return torch.float64 if t.dtype == torch.float64 else torch.float
 
 
 def _sq(v: torch.Tensor) -> torch.Tensor:
@@ -246,7 +257,7 @@ class Stepper:
             A, A2 = st.S['h'].clone().detach(), st.x
             w2 = st.W[f'x2{q}'].clone().detach()
 
-        grad = torch.zeros_like(w, dtype=torch.float)
+        grad = torch.zeros_like(w, dtype=_wide(w))
         for t in range(1, T + 1):
             at, ot = A[:, t - 1, :], A2[:, t - 1, :]
             z = at @ w + ot @ w2
@@ -256,7 +267,7 @@ class Stepper:
         grad = grad * rq
 
         def f(b):
-            acc = torch.tensor(0., dtype=torch.float)
+            acc = torch.zeros((), dtype=_wide(w), device=w.device)
             for t in range(1, T + 1):
                 at, ot = A[:, t - 1, :], A2[:, t - 1, :]
                 acc += 0.5 * self._r(q) * _sq(
@@ -411,3 +422,29 @@ class Stepper:
         T = st.T
         hw = self._slice(st.S, 'h', T) @ st.W['out'].clone().detach()
         st.L['y'] = (st.L['y'].clone().detach() + self._r('y') * (st.S['a'].clone().detach() - hw)).clone().detach()
+
+
+# ----------------------------------------------------------------------------- fp64 arbitration
+
+def fp64_decisions(x, y, W, S, L, hyper: Hyper, global_batch: Optional[int] = None,
+                   device: Optional[torch.device] = None) -> dict:
+    """ONE step of the restatement above in fp64 from the given (fp32) state, for its
+    line-search decisions only: the arbiter of the GPU parity tests and of the golden
+    fixtures' ``fp64`` records.
+
+    The reference decides ``f(W + G/2^k) > est`` in fp32 (admm.py:331-336), where both sides
+    are sums of ~1e3 that differ in the 7th-8th digit at the exponents taken at C3-like sizes:
+    its k there is rounding noise.  In fp64 the same comparisons have ~9 more digits.  Returns
+    ``{'weights': [(name, k, margin)], 'theta_h': theta}`` in step order, where margin = the
+    smallest |f(beta) - est| / |est - f(W)| of the deciding comparisons (the last failing
+    one and the passing one): decisions with margin below ~1e-6 are ties even in fp64."""
+    dev = device or x.device
+    d = lambda m: {k: v.detach().to(dev, torch.float64) for k, v in m.items()}  # noqa: E731
+    st = State(x.to(dev, torch.float64), y.to(dev, torch.float64), d(W), d(S), d(L),
+               global_batch or x.shape[0])
+    rec = Stepper(hyper.cast(torch.float64), trace_fw=True).step(st)
+    out = []
+    for r in rec['weights']:
+        ms = [abs(a - b) / abs(b - r['f_w']) for a, b, _ in r['tests'][-2:] if b != r['f_w']]
+        out.append((r['name'], r['k'], min(ms) if ms else float('inf')))
+    return {'weights': out, 'theta_h': rec['hT']['theta'] if rec['hT'] else None}

@@ -57,7 +57,18 @@ CASES = {
     't2_c2_nd_rw':  ('no_dual_y', False, 'rw', 1024, 16, 1, 64, 6, False, 'GoogleStock'),
     # C1: the real GoogleStock windows (demo.py defaults: hidden 10, 30 epochs), train + val losses
     'c1_goog':      ('admm', False, 'goog', 4224, 10, 1, 10, 30, False, 'GoogleStock'),
+    # BASELINE configs at full size (compact: inputs as generator recipe + sha256, no state)
+    'c3':           ('admm', False, 'uniform', 8192, 32, 16, 256, 5, False, 'GoogleStock'),
+    'c5_1gpu':      ('no_dual_y', False, 'rw', 4096, 64, 1, 512, 3, False, 'GoogleStock'),
 }
+
+# compact cases: which steps keep their full weights (the others keep x2q/out in full and
+# every WSTRIDE-th entry of h2q), and whether each pre-step reference state is also stepped
+# once by the fp64 oracle (oracle.admm_oracle.fp64_decisions) to record how the reference's
+# fp32 line-search decisions compare with fp64 ones from the same state
+COMPACT = {'c3': {'full_w': (1, 2, 3, 4, 5), 'fp64': True},
+           'c5_1gpu': {'full_w': (3,), 'fp64': False}}
+WSTRIDE = 16
 
 
 def goog_windows():
@@ -154,9 +165,16 @@ def run_case(name):
     x, y = make_inputs(gen, B, T, D)
     torch.manual_seed(0)
     model = LSTM(D, H, 1)
-    arrays = {'x': x.numpy(), 'y': y.numpy()}
-    for w in WNAMES:
-        arrays[f'w0_{w}'] = getattr(model, w).detach().numpy().copy()
+    compact = COMPACT.get(name)
+    arrays = {} if compact else {'x': x.numpy(), 'y': y.numpy()}
+    if not compact:
+        for w in WNAMES:
+            arrays[f'w0_{w}'] = getattr(model, w).detach().numpy().copy()
+    fp64_recs = []
+    if compact and compact['fp64']:
+        sys.path.insert(0, os.path.dirname(os.path.dirname(OUT)))
+        from oracle import admm_oracle as O
+        hyper = O.Hyper.from_dict(pdict, variant, dual_y)
     loss_fn = torch.nn.MSELoss()
 
     def loss():
@@ -187,6 +205,13 @@ def run_case(name):
     val_losses = [val_loss()]
     searches, step_times = [], []
     for s in range(1, steps + 1):
+        if compact and compact['fp64']:
+            t0 = time.time()
+            W = {w: getattr(model, w).detach() for w in WNAMES}
+            dec = O.fp64_decisions(x, y, W, opt.gates, opt.duals, hyper)
+            fp64_recs.append({'k': [k for _, k, _ in dec['weights']], 'margin': [m for _, _, m in dec['weights']],
+                              'theta_h': dec['theta_h']})
+            print(f'{name}: fp64 decisions before step {s}: {fp64_recs[-1]["k"]} ({time.time() - t0:.1f}s)', flush=True)
         with GtRecorder() as rec:
             t0 = time.time()
             opt.step()
@@ -204,7 +229,10 @@ def run_case(name):
             'c_count': sum(len(srch) for srch in c_s),
         })
         for w in WNAMES:
-            arrays[f'w{s}_{w}'] = getattr(model, w).detach().numpy().copy()
+            v = getattr(model, w).detach().numpy().copy()
+            if compact and s not in compact['full_w'] and w.startswith('h2'):
+                v = v.reshape(-1)[::WSTRIDE].copy()
+            arrays[f'w{s}_{w}'] = v
         if full:
             snap_state(f's{s}')
         losses.append(loss())
@@ -218,6 +246,13 @@ def run_case(name):
         'torch': torch.__version__, 'threads': torch.get_num_threads(), 'step_times': step_times,
         'generator': 'tests/golden/make_golden.py',
     }
+    if compact:
+        import hashlib
+        meta['compact'] = {'full_w': list(compact['full_w']), 'wstride': WSTRIDE,
+                           'x_sha256': hashlib.sha256(x.numpy().tobytes()).hexdigest(),
+                           'y_sha256': hashlib.sha256(y.numpy().tobytes()).hexdigest(),
+                           'inputs': f'make_inputs({gen!r}, {B}, {T}, {D}) (SURVEY.md 8(d) generator)'}
+        meta['fp64'] = fp64_recs
     arrays['meta_json'] = np.array(json.dumps(meta))
     path = os.path.join(OUT, f'{name}.npz')
     np.savez_compressed(path, **arrays)

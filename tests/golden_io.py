@@ -1,4 +1,9 @@
-"""Loading helpers for the golden fixtures in tests/golden/ (data only, no pickles)."""
+"""Loading helpers for the golden fixtures in tests/golden/ (data only, no pickles).
+
+Compact fixtures (the BASELINE configs at full size: ``c3``, ``c5_1gpu``) hold no input
+arrays: their inputs are regenerated from SURVEY.md 8(d)'s seeded generators and checked
+against the sha256 recorded when the reference ran on them."""
+import hashlib
 import json
 import os
 
@@ -26,15 +31,38 @@ class Golden:
         return torch.from_numpy(self.z[key].copy())
 
     @property
+    def compact(self):
+        return self.meta.get('compact')
+
+    def _inputs(self):
+        if 'xy' not in self.__dict__:
+            if self.compact:
+                x, y = make_inputs(self.gen, self.B, self.T, self.D)
+                for v, key in ((x, 'x_sha256'), (y, 'y_sha256')):
+                    assert hashlib.sha256(v.numpy().tobytes()).hexdigest() == self.compact[key], (self.name, key)
+            else:
+                x, y = self.t('x'), self.t('y')
+            self.__dict__['xy'] = (x, y)
+        return self.__dict__['xy']
+
+    @property
     def x(self):
-        return self.t('x')
+        return self._inputs()[0]
 
     @property
     def y(self):
-        return self.t('y')
+        return self._inputs()[1]
 
     def weights(self, step):
         return {k: self.t(f'w{step}_{k}') for k in WEIGHT_NAMES}
+
+    def full_weights(self, step) -> bool:
+        return not self.compact or step in self.compact['full_w']
+
+    def fp64_ks(self, step):
+        """Compact fixtures with fp64 records: the fp64 oracle's exponents from the reference's
+        own state before ``step`` (1-based)."""
+        return self.meta['fp64'][step - 1]['k']
 
     def state(self, step):
         S = {q: self.t(f's{step}_S_{q}') for q in GATES6}
@@ -48,6 +76,25 @@ class Golden:
         return [len(v) - 1 for v in self.searches[step - 1]['weights']]
 
 
-# step fixtures (goog_cols45.npz holds the C1 input columns, not a step trajectory)
-ALL = sorted(f[:-4] for f in os.listdir(GOLDEN) if f.endswith('.npz') and not f.startswith('goog_'))
+def make_inputs(gen: str, B: int, T: int, D: int):
+    """SURVEY.md 8(d) synthetic inputs (the generators tests/golden/make_golden.py ran the
+    reference on): uniform (seed 1234) and random-walk windows (seed 7)."""
+    if gen == 'uniform':
+        g = torch.Generator().manual_seed(1234)
+        x = torch.rand(B, T, D, generator=g)
+        y = 0.8 * x.mean((1, 2)).unsqueeze(1) + 0.1 * torch.rand(B, 1, generator=g)
+        return x.contiguous(), y.contiguous()
+    assert gen == 'rw' and D == 1, gen
+    g = torch.Generator().manual_seed(7)
+    s = torch.cumsum(torch.randn(B + T + 1, generator=g), 0)
+    s = (s - s.min()) / (s.max() - s.min())
+    idx = torch.arange(B).unsqueeze(1) + torch.arange(T).unsqueeze(0)
+    return s[idx].unsqueeze(2).contiguous(), s[torch.arange(B) + T].unsqueeze(1).contiguous()
+
+
+# step fixtures (goog_cols45.npz holds the C1 input columns, not a step trajectory); the compact
+# full-size ones are run by their own tests
+_NAMES = sorted(f[:-4] for f in os.listdir(GOLDEN) if f.endswith('.npz') and not f.startswith('goog_'))
+COMPACT = [n for n in _NAMES if Golden(n).compact]
+ALL = [n for n in _NAMES if n not in COMPACT]
 FULL = [n for n in ALL if Golden(n).full_state]

@@ -34,6 +34,21 @@ def test_library_exports_every_declared_symbol():
     assert b'gfx950' in lib.admm_build_info()
 
 
+def test_create_rejects_unsupported_output_width():
+    """O is bounded only by the h_T kernels' LDS row (4 waves x O floats): O <= 4096.  Larger
+    widths fail in admm_create's argument check, before any device call, with a message."""
+    from admm_amd import _native as N
+    lib = N.load()
+    p = N.AdmmParams()
+    for i in range(7):
+        p.rho[i] = 1.0
+    ctx = ctypes.c_void_p()
+    d = N.AdmmDims(64, 64, 4, 3, 16, 5000)
+    rc = lib.admm_create(ctypes.byref(d), ctypes.byref(p), 0, ctypes.byref(ctx))
+    assert rc != 0 and not ctx.value
+    assert b'output_size 5000 > 4096' in lib.admm_last_error()
+
+
 def test_struct_layouts_match_header():
     from admm_amd import _native as N
     assert ctypes.sizeof(N.AdmmDims) == 32

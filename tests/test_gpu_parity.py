@@ -59,28 +59,14 @@ def _loss(model, x, y):
     return float(torch.nn.functional.mse_loss(model(x), y))
 
 
-def _fp64_step_decisions(g: Golden, W, S, L):
-    """(k, margin) of each weight search of ONE fp64 oracle step from the given fp32 state.
-    margin = smallest |f(beta) - est| / |est - f(W)| of the deciding comparisons (the last
-    failing one and the passing one)."""
-    torch.set_default_dtype(torch.float64)
-    orig = O._autograd
-    try:
-        hp = O.Hyper.from_dict(g.params, g.variant, g.with_dual_y)
-        hp.rho = {k: v.double() for k, v in hp.rho.items()}
-        hp.beta = {k: v.double() for k, v in hp.beta.items()}
-        d = lambda m: {k: v.double().cpu() for k, v in m.items()}  # noqa: E731
-        st = O.State(g.x.double(), g.y.double(), d(W), d(S), d(L), g.B)
-        O._autograd = lambda fn, at: (lambda v: (fn(v).backward(), v.grad)[1])(
-            at.clone().detach().requires_grad_(True))
-        dec = []
-        for r in O.Stepper(hp, trace_fw=True).step(st)['weights']:
-            ms = [abs(a - b) / abs(b - r['f_w']) for a, b, _ in r['tests'][-2:] if b != r['f_w']]
-            dec.append((r['k'], min(ms) if ms else math.inf))
-        return dec
-    finally:
-        O._autograd = orig
-        torch.set_default_dtype(torch.float32)
+def _fp64_step_decisions(g, W, S, L, device='cuda'):
+    """(k, margin) of each weight search of ONE fp64 oracle step from the given fp32 state
+    (oracle.admm_oracle.fp64_decisions, run on the GPU in fp64).  margin = smallest
+    |f(beta) - est| / |est - f(W)| of the deciding comparisons (the last failing one and the
+    passing one)."""
+    hp = O.Hyper.from_dict(g.params, g.variant, g.with_dual_y)
+    dec = O.fp64_decisions(g.x, g.y, W, S, L, hp, global_batch=g.B, device=torch.device(device))
+    return [(k, m) for _, k, m in dec['weights']]
 
 
 # c1_goog (real data) has noise-level reference decisions after step 15: checked per
@@ -310,10 +296,13 @@ def test_forward_matches_oracle(dev):
 
 
 @pytest.mark.parametrize('shape', [(200, 5, 3, 40, 2), (33, 1, 2, 7, 1), (129, 4, 5, 33, 3),
-                                   (100, 3, 5, 64, 1), (40, 1, 16, 32, 1), (64, 3, 4, 32, 1), (70, 3, 2, 96, 1)])
+                                   (100, 3, 5, 64, 1), (40, 1, 16, 32, 1), (64, 3, 4, 32, 1), (70, 3, 2, 96, 1),
+                                   (150, 3, 4, 24, 10), (70, 2, 16, 64, 13)])
 def test_edge_shapes_vs_oracle(shape, mods, dev):
-    """Ragged tiles (B, H not multiples of 128/32), T = 1, multi-output O.  H % 32 == 0 runs the
-    persistent sweep (k_sweep_rows) with a ragged last row block; the others the per-t sweep."""
+    """Ragged tiles (B, H not multiples of 128/32), T = 1, multi-output O (O = 10, 13: more
+    output columns than one pass of the generic h_T kernels holds, kOChunk = 8).  H % 32 == 0
+    runs the persistent sweep (k_sweep_rows) with a ragged last row block; the others the per-t
+    sweep."""
     from blocks.lstm import LSTM
     from parameters import example_parameter_dictionary
     admm, _ = mods

@@ -98,6 +98,12 @@ __device__ __forceinline__ void split3(V a, B& p0, B& p1, B& p2) {
   const V r2 = r1 - bf16_widen<V>(p1);
   p2 = __builtin_convertvector(r2, B);
 }
+// two-way split a = p0 + p1 (to ~2^-17 relative): the first two pieces of split3
+template <class V, class B>
+__device__ __forceinline__ void split2(V a, B& p0, B& p1) {
+  p0 = __builtin_convertvector(a, B);
+  p1 = __builtin_convertvector(a - bf16_widen<V>(p0), B);
+}
 __device__ __forceinline__ void split3(float a, __bf16& p0, __bf16& p1, __bf16& p2) {
   p0 = (__bf16)a;
   const float r1 = a - (float)p0;

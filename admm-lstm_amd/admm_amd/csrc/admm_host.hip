@@ -123,6 +123,10 @@ struct AdmmCtx {
   // enters the line-search increments, where 2^-16 relative is far inside the reference's own
   // rounding of W + G/theta (DESIGN.md "trial direction precision"); G itself stays split3.
   int q_pieces = 2;
+  // split pieces of the h-side gradient G_h = rho Hprev^T R (k_atr3w): 2 = the three products of
+  // two-way splits, ~2^-16 relative per product -- the accuracy of the reference's own fp32 sums of
+  // B*T terms (DESIGN.md "h-side gradient on two-way splits"); ADMM_ATR_PIECES=3: f32-accurate split3
+  int atr_pieces = 2;
   bool atr3w = true;
   // Q in the row-quad layout (k_qgemm3 -> k_trial_rows<1>; ADMM_QPAIR=0: row-major)
   bool qpair = true;       // k_atr3w (two waves per SIMD) for the h-side gradient; ADMM_ATR3W=0: k_atr3
@@ -150,6 +154,8 @@ struct AdmmCtx {
   uint32_t prof_mask = 0;
   std::vector<hipEvent_t> ev_pool;
   std::vector<std::pair<int, std::pair<hipEvent_t, hipEvent_t>>> ev_used;
+  // admm_debug_trace: caller buffers receiving each stage's G (tests)
+  float* trace_g[2] = {nullptr, nullptr};
 };
 
 namespace {
@@ -277,7 +283,7 @@ int stage_weights(AdmmCtx* c, int side, hipStream_t s) {
   } else if (fast && c->split3) {
     ns = atr3_splits(g);
     ProfScope ps(c, ADMM_PROF_ATR_H, s);
-    launch_atr3(g, c->buf.gates[ADMM_H], zh, c->tgt, c->gslab, ns, s, c->atr3w);
+    launch_atr3(g, c->buf.gates[ADMM_H], zh, c->tgt, c->gslab, ns, s, c->atr3w, c->atr_pieces);
   } else if (fast) {
     ns = atr_splits(g, 1);
     ProfScope ps(c, ADMM_PROF_ATR_H, s);
@@ -304,6 +310,8 @@ int stage_weights(AdmmCtx* c, int side, hipStream_t s) {
   launch_reduce_g(g, side, c->hp, gsrc, ns, c->G, c->found, spec && side == 0 ? c->kpred : nullptr, c->stats, s);
   int rc = allreduce_f32(c, c->G, (size_t)4 * Kd * g.H, s);
   if (rc) return rc;
+  if (c->trace_g[side])
+    HIP_TRY(hipMemcpyAsync(c->trace_g[side], c->G, (size_t)4 * Kd * g.H * sizeof(float), hipMemcpyDeviceToDevice, s));
   // 2. trial direction Q = A G (not needed on the fast x side: formed inside the trials)
   if (!(fast && side == 0)) {
     ProfScope ps(c, side == 0 ? ADMM_PROF_QGEMM_X : ADMM_PROF_QGEMM_H, s);
@@ -486,7 +494,8 @@ int admm_create(const AdmmDims* dims, const AdmmParams* params, int device, Admm
   if (const char* e = std::getenv("ADMM_SPLIT3")) c->split3 = c->split3 && std::atoi(e) != 0;
   if (const char* e = std::getenv("ADMM_ATR3W")) c->atr3w = std::atoi(e) != 0;
   if (const char* e = std::getenv("ADMM_QPAIR")) c->qpair = std::atoi(e) != 0;
-  if (const char* e = std::getenv("ADMM_Q_PIECES")) c->q_pieces = std::atoi(e) == 2 ? 2 : 3;
+  if (const char* e = std::getenv("ADMM_Q_PIECES")) c->q_pieces = std::max(1, std::min(3, std::atoi(e)));
+  if (const char* e = std::getenv("ADMM_ATR_PIECES")) c->atr_pieces = std::atoi(e) == 2 ? 2 : 3;
   Hyper& h = c->hp;
   for (int i = 0; i < 7; ++i) h.rho[i] = params->rho[i];
   h.rinv_exact = 1;
@@ -784,6 +793,13 @@ int admm_debug_workspace(AdmmCtx* c, int32_t which, void* dst, int64_t bytes, vo
   HIP_TRY(hipMemcpyAsync(dst, src, need, hipMemcpyDeviceToDevice, s));
   HIP_TRY(hipStreamSynchronize(s));
   return which == 0 ? (c->z_valid ? 1 : 0) : (c->tgt_valid && c->z_valid ? 1 : 0);
+}
+
+int admm_debug_trace(AdmmCtx* c, float* gx, float* gh) {
+  if (!c) return fail(ADMM_EINVAL, "NULL ctx");
+  c->trace_g[0] = gx;
+  c->trace_g[1] = gh;
+  return ADMM_OK;
 }
 
 int admm_debug_trial(const float* z, const float* tgt, const float* q, int64_t n, int32_t tanh_gate, int32_t kbase,

@@ -205,7 +205,7 @@ int atr3_splits(const Geom& g);
 // k_atr3's 4 with 256; the same products in the same order, so bit-identical slabs
 bool atr3w_ok(const Geom& g);
 void launch_atr3(const Geom& g, const float* Sh, const float* zc, const float* tgt, float* slab, int nsplit,
-                 hipStream_t s, bool two_waves = true);
+                 hipStream_t s, bool two_waves = true, int pieces = 3);
 // pieces = 3: f32-accurate split3 products; 2: two-way splits, three products (~2^-16 relative),
 // enough for the trial direction ("trial direction precision")
 // qpair (and qpair_ok: BT % 4 == 0): Q in the row-quad layout [q][row / 4][j][row % 4] that

@@ -328,8 +328,12 @@ constexpr int A3W_THREADS = 512;
 #endif
 struct Atr3wRing { float4 a[2], z[2], t[2]; };
 
-// (mb, nb): the 256 x 256 block of G_q (H_prev columns 256 mb.., R columns 256 nb..)
-template <bool TANH>
+// (mb, nb): the 256 x 256 block of G_q (H_prev columns 256 mb.., R columns 256 nb..).
+// NP = 3: split3 operands, six products (f32-accurate); NP = 2: two-way splits, the three
+// products of mfma_split2 (~2^-16 relative per product, the accuracy of the reference's own fp32
+// sums over B*T rows; DESIGN.md "h-side gradient on two-way splits"), half the matrix work and
+// two thirds of the staging
+template <bool TANH, int NP>
 __device__ __forceinline__ void atr3w_body(const Geom& g, int q, int sp, int nsplit, int mb, int nb,
                                            const float* __restrict__ Sh, const float* __restrict__ zq,
                                            const float* __restrict__ tq, float* __restrict__ slab, __bf16* img) {
@@ -360,18 +364,23 @@ __device__ __forceinline__ void atr3w_body(const Geom& g, int q, int sp, int nsp
       R.t[i] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rT, vz, (int)(row * H * 4), 2));
     }
   };
+  constexpr int STAGE = NP * (P::PA + P::PR);
   auto put = [&](int st, const Atr3wRing& R, int64_t k0) {
-    __bf16* A = img + st * P::STAGE;
-    __bf16* B = A + 3 * P::PA;
+    __bf16* A = img + st * STAGE;
+    __bf16* B = A + NP * P::PA;
     bf16x4 p0, p1, p2;
+    auto pieces = [&](f32x4 v) {
+      if constexpr (NP == 3) split3(v, p0, p1, p2);
+      else split2(v, p0, p1);
+    };
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const int rr = 2 * rg + i;
       const int o = a3_off(rr, 4 * lane);
-      split3(f32x4{R.a[i].x, R.a[i].y, R.a[i].z, R.a[i].w}, p0, p1, p2);
+      pieces(f32x4{R.a[i].x, R.a[i].y, R.a[i].z, R.a[i].w});
       *reinterpret_cast<bf16x4*>(A + o) = p0;
       *reinterpret_cast<bf16x4*>(A + P::PA + o) = p1;
-      *reinterpret_cast<bf16x4*>(A + 2 * P::PA + o) = p2;
+      if constexpr (NP == 3) *reinterpret_cast<bf16x4*>(A + 2 * P::PA + o) = p2;
       const bool ok = k0 + rr < r1;
       const float zz[4] = {R.z[i].x, R.z[i].y, R.z[i].z, R.z[i].w};
       const float tt[4] = {R.t[i].x, R.t[i].y, R.t[i].z, R.t[i].w};
@@ -382,10 +391,10 @@ __device__ __forceinline__ void atr3w_body(const Geom& g, int q, int sp, int nsp
         phi_fast<TANH>(zz[u], phi, dphi);
         rv[u] = ok ? (phi - tt[u]) * dphi : 0.f;
       }
-      split3(rv, p0, p1, p2);
+      pieces(rv);
       *reinterpret_cast<bf16x4*>(B + o) = p0;
       *reinterpret_cast<bf16x4*>(B + P::PR + o) = p1;
-      *reinterpret_cast<bf16x4*>(B + 2 * P::PR + o) = p2;
+      if constexpr (NP == 3) *reinterpret_cast<bf16x4*>(B + 2 * P::PR + o) = p2;
     }
   };
   // transposed fragment reads (k_atr3's lane map)
@@ -394,7 +403,7 @@ __device__ __forceinline__ void atr3w_body(const Geom& g, int q, int sp, int nsp
   auto frag = [&](const __bf16* O, int piece, int cbase, bf16x8 (&f)[3]) {
     const int o0 = a3_off(frow, cbase + fcol), o1 = a3_off(frow + 4, cbase + fcol);
 #pragma unroll
-    for (int p = 0; p < 3; ++p) {
+    for (int p = 0; p < NP; ++p) {
       typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
       const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(O + p * piece + o0));
       const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(O + p * piece + o1));
@@ -405,8 +414,8 @@ __device__ __forceinline__ void atr3w_body(const Geom& g, int q, int sp, int nsp
   f32x16 acc[4][2];
   zero_acc(acc);
   auto compute = [&](int st) {
-    const __bf16* A = img + st * P::STAGE;
-    const __bf16* B = A + 3 * P::PA;
+    const __bf16* A = img + st * STAGE;
+    const __bf16* B = A + NP * P::PA;
     bf16x8 b[2][3];
 #pragma unroll
     for (int ni = 0; ni < 2; ++ni) frag(B, P::PR, wc * 64 + ni * 32, b[ni]);
@@ -417,7 +426,8 @@ __device__ __forceinline__ void atr3w_body(const Geom& g, int q, int sp, int nsp
 #pragma unroll
       for (int ni = 0; ni < 2; ++ni) {
         if (A3W_ABL & 2) acc[mi][ni][0] += (float)a[0][0] * (float)b[ni][0][0];   // ablation: no MFMAs
-        else acc[mi][ni] = mfma_split3(a, b[ni], acc[mi][ni]);
+        else if constexpr (NP == 3) acc[mi][ni] = mfma_split3(a, b[ni], acc[mi][ni]);
+        else acc[mi][ni] = mfma_split2(a, b[ni], acc[mi][ni]);
       }
     }
   };
@@ -452,17 +462,18 @@ __device__ __forceinline__ void atr3w_body(const Geom& g, int q, int sp, int nsp
     }
 }
 
+template <int NP>
 __global__ __launch_bounds__(A3W_THREADS, 1) void k_atr3w(Geom g, const float* __restrict__ Sh,
                                                          const float* __restrict__ zc, const float* __restrict__ tgt,
                                                          float* __restrict__ slab, int nsplit) {
-  __shared__ __attribute__((aligned(16))) __bf16 img[2 * A3<256>::STAGE];
+  __shared__ __attribute__((aligned(16))) __bf16 img[2 * NP * (A3<256>::PA + A3<256>::PR)];
   int lid = xcd_swizzle(blockIdx.x, gridDim.x);
   const int q = lid % 4;          // the 4 gates of one split share the Hprev rows: same XCD
   lid /= 4;
   const int nt = g.H / 256, tl = lid % (nt * nt), sp = lid / (nt * nt);
   const int64_t n = g.BT() * g.H;
-  if (q == 2) atr3w_body<true>(g, q, sp, nsplit, tl / nt, tl % nt, Sh, zc + q * n, tgt + q * n, slab, img);
-  else atr3w_body<false>(g, q, sp, nsplit, tl / nt, tl % nt, Sh, zc + q * n, tgt + q * n, slab, img);
+  if (q == 2) atr3w_body<true, NP>(g, q, sp, nsplit, tl / nt, tl % nt, Sh, zc + q * n, tgt + q * n, slab, img);
+  else atr3w_body<false, NP>(g, q, sp, nsplit, tl / nt, tl % nt, Sh, zc + q * n, tgt + q * n, slab, img);
 }
 
 }  // namespace
@@ -484,11 +495,12 @@ int atr3_splits(const Geom& g) {
 bool atr3w_ok(const Geom& g) { return g.H % 256 == 0; }
 
 void launch_atr3(const Geom& g, const float* Sh, const float* zc, const float* tgt, float* slab, int nsplit,
-                 hipStream_t s, bool two_waves) {
+                 hipStream_t s, bool two_waves, int pieces) {
   dim3 grid((g.H / A3_BM) * (g.H / A3_BN) * 4 * nsplit);
   if (two_waves && atr3w_ok(g)) {   // 256 x 256 blocks of each gate's G, nsplit row ranges
     const int nt = g.H / 256;
-    k_atr3w<<<4 * nt * nt * nsplit, A3W_THREADS, 0, s>>>(g, Sh, zc, tgt, slab, nsplit);
+    if (pieces == 2) k_atr3w<2><<<4 * nt * nt * nsplit, A3W_THREADS, 0, s>>>(g, Sh, zc, tgt, slab, nsplit);
+    else k_atr3w<3><<<4 * nt * nt * nsplit, A3W_THREADS, 0, s>>>(g, Sh, zc, tgt, slab, nsplit);
   } else {
     k_atr3<<<grid, kThreads, 0, s>>>(g, Sh, zc, tgt, slab, nsplit);
   }
@@ -512,10 +524,12 @@ void launch_qgemm3_img(const Geom& g, const float* Sh, const float* gimg, float*
 #endif
   const bf16x8* gb = reinterpret_cast<const bf16x8*>(gimg);
   qpair = qpair && qpair_ok(g);
-  const int BM = pieces == 2 ? Q3_BM2 : 128;
+  const int BM = pieces == 2 ? Q3_BM2 : 128;   // (pieces 1: 128)
   const int64_t nrt = (g.BT() + BM - 1) / BM;
   dim3 grid((unsigned)(nrt * 4 * (g.H / Q3_BN)));
-  if (pieces == 2 && qpair) k_qgemm3<2, true, Q3_BM2><<<grid, 2 * Q3_BM2, 0, s>>>(g, Sh, gb, Q, found);
+  if (pieces == 1 && qpair) k_qgemm3<1, true, 128><<<grid, 256, 0, s>>>(g, Sh, gb, Q, found);
+  else if (pieces == 1) k_qgemm3<1, false, 128><<<grid, 256, 0, s>>>(g, Sh, gb, Q, found);
+  else if (pieces == 2 && qpair) k_qgemm3<2, true, Q3_BM2><<<grid, 2 * Q3_BM2, 0, s>>>(g, Sh, gb, Q, found);
   else if (pieces == 2) k_qgemm3<2, false, Q3_BM2><<<grid, 2 * Q3_BM2, 0, s>>>(g, Sh, gb, Q, found);
   else if (qpair) k_qgemm3<3, true, 128><<<grid, 256, 0, s>>>(g, Sh, gb, Q, found);
   else k_qgemm3<3, false, 128><<<grid, 256, 0, s>>>(g, Sh, gb, Q, found);

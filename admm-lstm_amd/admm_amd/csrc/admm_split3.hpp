@@ -66,7 +66,9 @@ constexpr int kQ3BU = (Q3_BN / 32) * 3 * 64;    // bf16x8 units of one B step im
 template <int BM>
 constexpr int Q3Lds() { return 2 * 3 * (BM * 16) * 2 + 2 * kQ3BU * 16; }
 
-// NP = 3: the six split3 products (f32-accurate); NP = 2: mfma_split2 (half the matrix work).
+// NP = 3: the six split3 products (f32-accurate); NP = 2: mfma_split2 (half the matrix work);
+// NP = 1: Hprev in two pieces, G in one (a0 b0 + a1 b0: G rounded to bf16, ~2^-9 relative per
+// element -- the trial direction only; a third of the B image and of the matrix work of NP = 3)
 template <int NP, int BM>
 __device__ __forceinline__ void qgemm3_tile(const Geom& g, const float* __restrict__ Sh,
                                             const bf16x8* __restrict__ gi, int q, int cb, int64_t m0,
@@ -74,7 +76,7 @@ __device__ __forceinline__ void qgemm3_tile(const Geom& g, const float* __restri
   // B image per step: NP = 3 all three pieces of each 32-column tile (192 units), NP = 2 only
   // pieces 0 and 1 (128 units): the third piece is never multiplied there
   constexpr int NT = 2 * BM;   // threads
-  constexpr int AP = BM * 16, PSTR = NP == 3 ? 192 : 128, BU = (Q3_BN / 32) * PSTR;
+  constexpr int AP = BM * 16, PSTR = NP == 3 ? 192 : NP == 2 ? 128 : 64, BU = (Q3_BN / 32) * PSTR;
   static_assert(BU % NT == 0, "B image units per thread");
   __bf16* As = reinterpret_cast<__bf16*>(lds);                       // [2][3 * AP]
   bf16x8* Bs = reinterpret_cast<bf16x8*>(lds + 2 * 3 * AP * 2);       // [2][BU]
@@ -101,12 +103,12 @@ __device__ __forceinline__ void qgemm3_tile(const Geom& g, const float* __restri
 #pragma unroll
     for (int u = 0; u < BU / NT; ++u) {
       const int i = tid + u * NT;   // image unit -> G-image unit (skipping piece 2 for NP = 2)
-      const int src = NP == 3 ? i : (i >> 7) * 192 + (i & 127);
+      const int src = NP == 3 ? i : NP == 2 ? (i >> 7) * 192 + (i & 127) : (i >> 6) * 192 + (i & 63);
       r.b[u] = bp[c * bstep + src - tid];
     }
   };
   auto lstore = [&](int st, const Slot& r) {
-    put3<NP>(As + st * 3 * AP, AP, sw_off(sr, sh), f32x8{r.a0.x, r.a0.y, r.a0.z, r.a0.w, r.a1.x, r.a1.y, r.a1.z, r.a1.w});
+    put3<NP == 1 ? 2 : NP>(As + st * 3 * AP, AP, sw_off(sr, sh), f32x8{r.a0.x, r.a0.y, r.a0.z, r.a0.w, r.a1.x, r.a1.y, r.a1.z, r.a1.w});
 #pragma unroll
     for (int u = 0; u < BU / NT; ++u) Bs[st * BU + tid + u * NT] = r.b[u];
   };
@@ -125,10 +127,20 @@ __device__ __forceinline__ void qgemm3_tile(const Geom& g, const float* __restri
 #pragma unroll
       for (int ni = 0; ni < 4; ++ni) {
         const bf16x8* bb = &Bs[st * BU + (wc * 4 + ni) * PSTR + lane];
+        if constexpr (NP == 1) {
+          const bf16x8 b0 = bb[0];
+          if (S3_ABL & 64) acc[mi][ni][0] += (float)a[0][0] * (float)b0[0];
+          else {
+            acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], b0, acc[mi][ni], 0, 0, 0);
+            acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b0, acc[mi][ni], 0, 0, 0);
+          }
+          continue;
+        } else {
         const bf16x8 b[3] = {bb[0], bb[64], NP == 3 ? bb[128] : bb[0]};
         if (S3_ABL & 64) acc[mi][ni][0] += (float)a[0][0] * (float)b[0][0];
         else if (NP == 3) acc[mi][ni] = mfma_split3(a, b, acc[mi][ni]);
         else acc[mi][ni] = mfma_split2(a, b, acc[mi][ni]);
+        }
       }
     }
   };

@@ -47,6 +47,8 @@ CONFIGS = {
     'c2': (2048, 16, 16, 64, 'admm', 'uniform'),
     'c3': (8192, 32, 16, 256, 'admm', 'uniform'),
     'c5': (4096, 64, 1, 512, 'no_dual_y', 'rw'),
+    # diagnostic: C4's global batch on one GPU (the line-search exponents of the 8-GPU run)
+    'c4g': (65536, 32, 16, 256, 'admm', 'uniform'),
 }
 
 
@@ -384,6 +386,7 @@ def main():
             'cpu_baseline': cpu,
             'kernels': kernel_ms,
             'line_search_k': list(stats['k'].values()),
+            'trial_passes': stats['passes'],
             'direct_frac': [round(v, 4) for v in stats['direct_frac'].values()],
             'final_train_mse': loss,
         }

@@ -188,6 +188,13 @@ int admm_debug_trial(const float* z, const float* tgt, const float* q, int64_t n
    return value's sign: 1 if the next x stage will read it, 0 if it will recompute it). */
 int admm_debug_workspace(AdmmCtx* ctx, int32_t which, void* dst, int64_t bytes, void* stream);
 
+/* Test hook: while set, every admm_step copies each weight stage's gradient G_q (rho-scaled,
+   after the all-reduce: the search direction of admm.py:302-312) on the step's stream into the
+   caller's device buffers: gx [4][D][H] (x stage), gh [4][H][H] (h stage).  NULL pointers
+   turn the copy off.  The parity tests use it to arbitrate line-search exponents from the
+   library's own search direction. */
+int admm_debug_trace(AdmmCtx* ctx, float* gx, float* gh);
+
 /* LSTM.forward / init_gate_variables (blocks/lstm.py:43-46, 65-88) without a context.
    x [B,T,D]; wx/wh/wy as above; out_a [B,O].  If gates_out is non-NULL it holds six
    [B,T+1,H] tensors that receive i,f,g,o,c,h at t >= 1 (their time-0 slices are the

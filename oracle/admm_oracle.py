@@ -294,6 +294,7 @@ class Stepper:
         rec = {'name': name, 'k': len(tests) - 1, 'tests': tests}
         if self.trace_fw:
             rec['f_w'] = float(f(w))
+            rec['grad'] = grad
         return rec
 
     # -- i, f, g, o closed forms (admm.py:353-386)
@@ -447,4 +448,34 @@ def fp64_decisions(x, y, W, S, L, hyper: Hyper, global_batch: Optional[int] = No
     for r in rec['weights']:
         ms = [abs(a - b) / abs(b - r['f_w']) for a, b, _ in r['tests'][-2:] if b != r['f_w']]
         out.append((r['name'], r['k'], min(ms) if ms else float('inf')))
-    return {'weights': out, 'theta_h': rec['hT']['theta'] if rec['hT'] else None}
+    return {'weights': out, 'theta_h': rec['hT']['theta'] if rec['hT'] else None,
+            'grads': [r['grad'] for r in rec['weights']]}
+
+
+def fp64_search(q: str, z, tgt, A, G, rho: float, T: int, kmax: int = 64):
+    """The backtracking search of ``admm.py:316-343`` for ONE gate weight, in fp64, from given
+    inputs: z [R, H] the pre-activations at W, tgt [R, H] = dual/rho + gate, A [R, K] the rows
+    of the side's input (X or H_prev), G [K, H] the (rho-scaled) gradient, i.e. the search
+    direction.  With beta - W = G/theta the test ``f(beta) > est(beta, theta)`` reads
+    ``0.5 rho sum[(phi(z + s A G) - tgt)^2 - (phi(z) - tgt)^2] > (1 + T/2) |G|^2 s``, s = 1/theta
+    (DESIGN.md section 2); the left side is summed as D (2 d0 + D), D = phi(z + s q) - phi(z),
+    without cancellation.  Given the GPU's own z, targets and G this isolates the line-search
+    arithmetic from the fp32 rounding of the state, which moves G itself (the arbiter of
+    ``tests/test_gpu_fullsize.py``).  Returns (k, margin) as ``fp64_decisions``."""
+    act = torch.tanh if q == 'g' else torch.sigmoid
+    z, tgt, A, G = (v.to(torch.float64) for v in (z, tgt, A, G))
+    p0 = act(z)
+    d0 = p0 - tgt
+    qd = A @ G
+    c = (1.0 + T / 2.0) * float((G * G).sum())
+    tests = []
+    for k in range(kmax):
+        s = 2.0 ** -k
+        D = act(z + qd * s) - p0
+        inc = 0.5 * rho * float((D * (2.0 * d0 + D)).sum())
+        est = c * s
+        tests.append((inc, est))
+        if not inc > est:
+            break
+    ms = [abs(a - b) / b for a, b in tests[-2:] if b > 0]
+    return len(tests) - 1, (min(ms) if ms else float('inf'))

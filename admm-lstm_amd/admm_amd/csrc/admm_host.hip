@@ -156,6 +156,9 @@ struct AdmmCtx {
   std::vector<std::pair<int, std::pair<hipEvent_t, hipEvent_t>>> ev_used;
   // admm_debug_trace: caller buffers receiving each stage's G (tests)
   float* trace_g[2] = {nullptr, nullptr};
+  // admm_debug_force: forced line-search decisions [8 exponents, h_T failing tests] (tests)
+  int* force_dev = nullptr;
+  bool force_on = false;
 };
 
 namespace {
@@ -330,6 +333,7 @@ int stage_weights(AdmmCtx* c, int side, hipStream_t s) {
   const bool fused_reduce = !c->comm && !c->host_ar;   // one process: k_select reduces the partials
   sa.pick = c->pick;
   sa.stats = c->stats;
+  sa.force = c->force_on ? c->force_dev : nullptr;
   const int nblk = fast ? stream_blocks(g) : c->nblk_trial;
   // the row-pair trial kernel (H % 256 == 0) writes one partial per (block, column block)
   const int nred = fast && side == 0 && trial_mx_ok(g) ? nblk * (g.H / 128)
@@ -424,7 +428,7 @@ int stage_sweep(AdmmCtx* c, hipStream_t s) {
   int rc = allreduce_f64(c, c->ht_sums, kHTSums, s);
   if (rc) return rc;
   launch_ht_apply(g, c->hp, sa.S, sa.L, c->buf.a, c->buf.dual_y, c->buf.y, c->buf.wy, c->ht_sums, c->stats,
-                  c->status_dev, s);
+                  c->status_dev, s, c->force_on ? c->force_dev : nullptr);
   return ADMM_OK;
 }
 
@@ -537,7 +541,7 @@ int admm_create(const AdmmDims* dims, const AdmmParams* params, int device, Admm
       (rc = dalloc(&c->found, 8)) || (rc = dalloc(&c->pick, 4)) ||
       (rc = dalloc(&c->U, (size_t)g.B * g.O)) || (rc = dalloc(&c->wy_slab, (size_t)c->wy_nsplit * g.H * g.O)) ||
       (rc = dalloc(&c->Gy, (size_t)g.H * g.O)) || (rc = dalloc(&c->ht_part, (size_t)c->ht_nblk * kHTSums)) ||
-      (rc = dalloc(&c->ht_sums, kHTSums)) || (rc = dalloc(&c->stats, 1)) || (rc = dalloc(&c->lamh_nz, 1)) ||
+      (rc = dalloc(&c->ht_sums, kHTSums)) || (rc = dalloc(&c->stats, 1)) || (rc = dalloc(&c->lamh_nz, 1)) || (rc = dalloc(&c->force_dev, 9)) ||
       (c->sweep_rows && (rc = dalloc(&c->swt, sweep_wt_floats(g)))) ||
       (c->split3 && (rc = dalloc(&c->gimg, split3_gimg_floats(g)))) ||
       (c->spec_x && ((rc = dalloc(&c->zx, 4 * plane)) || (rc = dalloc(&c->kpred, 4)))) ||
@@ -572,7 +576,7 @@ int admm_destroy(AdmmCtx* c) {
   if (!c) return ADMM_OK;
   DeviceGuard dg_(c->device);
   void* ptrs[] = {c->zc, c->tgt, c->R, c->Q, c->G, c->dW, c->gslab, c->tr_part, c->tr_sums, c->tr_poly, c->found, c->pick,
-                  c->U, c->wy_slab, c->Gy, c->ht_part, c->ht_sums, c->stats, c->swt, c->gimg, c->zx, c->kpred, c->gx_slab, c->lamh_nz};
+                  c->U, c->wy_slab, c->Gy, c->ht_part, c->ht_sums, c->stats, c->swt, c->gimg, c->zx, c->kpred, c->gx_slab, c->lamh_nz, c->force_dev};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   if (c->comm) ncclCommDestroy(c->comm);
@@ -799,6 +803,37 @@ int admm_debug_trace(AdmmCtx* c, float* gx, float* gh) {
   if (!c) return fail(ADMM_EINVAL, "NULL ctx");
   c->trace_g[0] = gx;
   c->trace_g[1] = gh;
+  return ADMM_OK;
+}
+
+int admm_debug_force(AdmmCtx* c, const int32_t* k8, int32_t ht_fails) {
+  if (!c) return fail(ADMM_EINVAL, "NULL ctx");
+  if (!k8) {
+    c->force_on = false;
+    return ADMM_OK;
+  }
+  int h[9];
+  for (int i = 0; i < 8; ++i) {
+    if (k8[i] < 0 || k8[i] >= kMaxK) return fail(ADMM_EINVAL, "admm_debug_force: k[%d] = %d out of [0, %d)", i, k8[i], kMaxK);
+    h[i] = k8[i];
+  }
+  if (ht_fails < 0 || ht_fails > kHTCand) return fail(ADMM_EINVAL, "admm_debug_force: ht_fails = %d", ht_fails);
+  h[8] = ht_fails;
+  DEVICE_GUARD(c->device);
+  HIP_TRY(hipDeviceSynchronize());   // the previous step may still read the old values
+  HIP_TRY(hipMemcpy(c->force_dev, h, sizeof h, hipMemcpyHostToDevice));
+  c->force_on = true;
+  return ADMM_OK;
+}
+
+int admm_debug_own(AdmmCtx* c, int32_t* k8, float* theta_h) {
+  if (!c || !k8 || !theta_h) return fail(ADMM_EINVAL, "admm_debug_own: NULL argument");
+  DEVICE_GUARD(c->device);
+  DevStats d;
+  HIP_TRY(hipDeviceSynchronize());
+  HIP_TRY(hipMemcpy(&d, c->stats, sizeof d, hipMemcpyDeviceToHost));
+  for (int i = 0; i < 8; ++i) k8[i] = d.k_own[i];
+  *theta_h = d.theta_h_own;
   return ADMM_OK;
 }
 

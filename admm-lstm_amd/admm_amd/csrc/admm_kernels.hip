@@ -1141,6 +1141,11 @@ __device__ __forceinline__ void direct_candidates(float sw, float e, float d2, f
   constexpr float kCap = 1e30f;
   float m = fminf(expm1_acc(-e), kCap);
   const float one_e = 1.f + E;
+  // the element's first-order term: D is linear in y = E expm1(-e) ~ -E e to first order, so
+  // D_lin = cr (-E e) r at the smallest candidate, doubling with e.  k_select compares the
+  // remainder past it, so its share 2 d0 D_lin / s goes into the s^1 polynomial coefficient
+  // (used from pass 0 only; the scale is pass 0's smallest candidate 2^-(J-1))
+  acc[kSlotPoly + 0] -= d2 * ((cr * (-E * e)) * r) * (float)(1 << (kTrialJ - 1));
   if (fabsf(e) * (float)(1 << (kTrialJ - 1)) <= 20.f) {   // |e| <= 20 on every candidate: no exp
 #pragma unroll
     for (int k = kTrialJ - 1; k >= 0; --k) {
@@ -1263,7 +1268,8 @@ __device__ __forceinline__ void trial_point(bool valid, float z, float tg, float
         const float q2 = qv * qv;
         const float a1 = c1 * qv, a2 = c2 * q2, a3 = c3 * q2 * qv, a4 = c4 * q2 * q2, a5 = c5 * q2 * q2 * qv;
         const float t = 2.f * d0;
-        acc[kSlotPoly + 0] += t * a1;
+        // (the first-order term t a1 is left out: the search compares the remainder past it,
+        // see k_select)
         acc[kSlotPoly + 1] += fmaf(t, a2, a1 * a1);
         acc[kSlotPoly + 2] += fmaf(t, a3, 2.f * a1 * a2);
         acc[kSlotPoly + 3] += fmaf(t, a4, fmaf(2.f * a1, a3, a2 * a2));
@@ -1351,7 +1357,8 @@ __device__ __forceinline__ void trial_pair(bool ok, f32x2 z, f32x2 tg, f32x2 qv,
     const f32x2 a1 = c1 * qp, a2 = a1 * gq, w3 = a1 * q2;
     const f32x2 a3 = w3 * k3, a4 = (w3 * gq) * k4, a5 = (w3 * q2) * k5;
     const f32x2 t = 2.f * d0, b1 = 2.f * a1, b2 = 2.f * a2, b3 = 2.f * a3, b4 = 2.f * a4;
-    acc2[1] = fma2(t, a1, acc2[1]);
+    // s^1 (acc2[1]): the first-order term t a1 is left out -- the search compares the remainder
+    // past it (k_select); the per-candidate elements subtract theirs in direct_candidates
     acc2[2] = fma2(a1, a1, fma2(t, a2, acc2[2]));
     acc2[3] = fma2(b1, a2, fma2(t, a3, acc2[3]));
     acc2[4] = fma2(a2, a2, fma2(b1, a3, fma2(t, a4, acc2[4])));
@@ -2139,7 +2146,13 @@ __global__ __launch_bounds__(kThreads) void k_trial_reduce(int pass, const doubl
 //     sums partials t, t + 256, ..., then the fixed wave / cross-wave tree of block_sum -- so
 //     every block holds bit-identical sums;
 //  2. computes ||G||^2 in the same fixed order;
-//  3. takes the first k with f(W + G/2^k) - f(W) <= (1 + T/2) ||G||^2 2^-k (admm.py:331-338):
+//  3. takes the first k with f(W + G/2^k) - f(W) <= (1 + T/2) ||G||^2 2^-k (admm.py:331-338),
+//     evaluated as the remainder past the first-order term: since G = grad f(W) (admm.py:302-312),
+//     f(W + s G) - f(W) = s <grad f, G> + r(s) with <grad f, G> = ||G||^2, and the test reads
+//     r(s) <= (T/2) ||G||^2 s.  The trial sums hold r directly (the per-element first-order terms
+//     2 d0 phi'(z) q s are left out of the polynomial and subtracted from the candidate sums), so
+//     the decision does not hinge on the rounding of d0 = phi(z) - tgt, which at C3 and C1 leaves
+//     O(1) relative noise in G and in s <grad f, G> alike.
 //     lhs_k = 0.5 rho (per-candidate sum of this window + polynomial part at s = 2^-k), in fp64;
 //  4. updates its slice of W <- (0.5 rho T theta* W - G) / (beta + 0.5 rho theta* T),
 //     theta* = 2^k / 2 (admm.py:338-343), and dW.
@@ -2245,13 +2258,16 @@ __global__ __launch_bounds__(kThreads) void k_select(Geom g, Hyper hp, SelectArg
       for (int n = kPolyN - 1; n >= 0; --n) poly = (poly + pl[n]) * sk;
       const double cand = poly_only ? 0.0 : sm[kk - k_lo];
       const double lhs = 0.5 * (double)rho * (cand + poly);
-      const double rhs = (1.0 + 0.5 * g.T) * gsq * sk;
+      const double rhs = 0.5 * g.T * gsq * sk;
       if (!isfinite(lhs) && mb == 0) atomicAdd(&a.stats->nonfinite, 1);
       if (lhs > rhs) continue;
       pick = kk;
       break;
     }
-    if (pick < 0 && (poly_only || a.pass == a.last_pass)) {
+    const int own = pick;   // -1: not decided within this pass's window
+    if (a.force) {          // test hook: take the given exponent (the search above still ran)
+      pick = a.force[2 * q + a.side];
+    } else if (pick < 0 && (poly_only || a.pass == a.last_pass)) {
       pick = k_hi;
       if (mb == 0) atomicAdd(&a.stats->unresolved, 1);
     }
@@ -2259,6 +2275,7 @@ __global__ __launch_bounds__(kThreads) void k_select(Geom g, Hyper hp, SelectArg
       if (pick >= 0) {
         const int slot = 2 * q + a.side;
         a.stats->k[slot] = pick;
+        if (a.force) a.stats->k_own[slot] = own;
         a.stats->f_w[slot] = 0.5 * (double)rho * sm[kSlotFw];
         a.stats->grad_sq[slot] = gsq;
         a.stats->direct_frac[slot] = sm[kSlotNne] / ((double)g.Bg * g.T * g.H);
@@ -2559,7 +2576,7 @@ __device__ __forceinline__ float ht_theta_star(const Hyper& hp, const double* su
 template <int OC>
 __global__ __launch_bounds__(kThreads) void k_ht_apply(Geom g, Hyper hp, Planes6 S, Planes6 L, float* a, float* Ly,
                                                          const float* y, const float* wy, const double* sums,
-                                                         DevStats* stats, int* status) {
+                                                         DevStats* stats, int* status, const int* force) {
   constexpr int CW = OC > 0 ? OC : kOChunk;
   const int NO = OC > 0 ? OC : g.O;
   extern __shared__ float ht_u[];
@@ -2567,9 +2584,13 @@ __global__ __launch_bounds__(kThreads) void k_ht_apply(Geom g, Hyper hp, Planes6
   const float ry = hp.rho[6], rh = hp.rho[5];
   const bool nd = hp.variant == 1;
   const bool shift = !nd && hp.with_dual_y;
-  const float th = ht_theta_star(hp, sums);
+  const float th_own = ht_theta_star(hp, sums);
+  // admm_debug_force: force[8] = the number of failing comparisons of the reference's search
+  // (theta = 0.1 doubled that many times, then halved: admm.py:474-482)
+  const float th = force ? ldexpf(0.1f, force[8]) / 2.f : th_own;
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     stats->theta_h = th;
+    stats->theta_h_own = th_own;
     if (status) {   // host-mapped mirror for admm_poll_status (the decide kernels ran earlier on this stream)
       __hip_atomic_store(&status[0], __hip_atomic_load(&stats->unresolved, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -2968,9 +2989,11 @@ void launch_ht_reduce(const double* part, int nblk, double* sums, hipStream_t s)
 }
 
 void launch_ht_apply(const Geom& g, const Hyper& hp, const Planes6& S, const Planes6& L, float* a, float* Ly,
-                     const float* y, const float* wy, const double* sums, DevStats* stats, int* status, hipStream_t s) {
-  if (g.O == 1) k_ht_apply<1><<<ht_blocks(g), kThreads, 0, s>>>(g, hp, S, L, a, Ly, y, wy, sums, stats, status);
-  else k_ht_apply<0><<<ht_blocks(g), kThreads, 4 * g.O * sizeof(float), s>>>(g, hp, S, L, a, Ly, y, wy, sums, stats, status);
+                     const float* y, const float* wy, const double* sums, DevStats* stats, int* status, hipStream_t s,
+                     const int* force) {
+  if (g.O == 1) k_ht_apply<1><<<ht_blocks(g), kThreads, 0, s>>>(g, hp, S, L, a, Ly, y, wy, sums, stats, status, force);
+  else k_ht_apply<0><<<ht_blocks(g), kThreads, 4 * g.O * sizeof(float), s>>>(g, hp, S, L, a, Ly, y, wy, sums, stats,
+                                                                            status, force);
 }
 
 }  // namespace admm

@@ -77,6 +77,10 @@ struct DevStats {
   double f_w[8];
   double grad_sq[8];
   double direct_frac[8];
+  // admm_debug_force: the exponents (and h_T theta) the step would have taken itself
+  int k_own[8];
+  float theta_h_own;
+  int pad2;
 };
 
 // ---- time step (one t): GEMM [x_t | h_{t-1}] @ [Wx; Wh] for the 4 gates + fused epilogue
@@ -232,6 +236,7 @@ struct SelectArgs {
   int* found_out;           // [4] decided after it (found + 4 ((pass + 1) & 1))
   int* pick;                // [4] exponent chosen in this pass, -1 if none
   DevStats* stats;
+  const int* force;         // [8] forced exponents per (gate, side) (admm_debug_force; nullable)
 };
 void launch_select(const Geom& g, const Hyper& hp, const SelectArgs& a, hipStream_t s);
 
@@ -250,6 +255,7 @@ void launch_ht_partial(const Geom& g, const Hyper& hp, const Planes6& S, const P
                        const float* Ly, const float* wy, double* part, int nblk, hipStream_t s);
 void launch_ht_reduce(const double* part, int nblk, double* sums, hipStream_t s);
 void launch_ht_apply(const Geom& g, const Hyper& hp, const Planes6& S, const Planes6& L, float* a, float* Ly,
-                     const float* y, const float* wy, const double* sums, DevStats* stats, int* status, hipStream_t s);
+                     const float* y, const float* wy, const double* sums, DevStats* stats, int* status, hipStream_t s,
+                     const int* force = nullptr);
 
 }  // namespace admm

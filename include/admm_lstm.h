@@ -195,6 +195,16 @@ int admm_debug_workspace(AdmmCtx* ctx, int32_t which, void* dst, int64_t bytes, 
    library's own search direction. */
 int admm_debug_trace(AdmmCtx* ctx, float* gx, float* gh);
 
+/* Test hook: replay given line-search decisions.  While set (k8 != NULL), every admm_step still
+   runs each search but then applies k8[2 q + side] (q = i,f,g,o; side 0 = x2q, 1 = h2q) as the
+   exponent of admm.py:331-343 and, for the h_T search (admm.py:474-482), theta = 0.1 doubled
+   ht_fails times, halved.  The decisions the step would have taken itself are read back with
+   admm_debug_own (k = -1: not decided within the first window of 16 exponents).  The parity
+   tests use it to follow a reference trajectory whose fp32 decisions are rounding noise
+   (C1 on GoogleStock) and to arbitrate the step's own decisions along it.  k8 == NULL: off. */
+int admm_debug_force(AdmmCtx* ctx, const int32_t* k8, int32_t ht_fails);
+int admm_debug_own(AdmmCtx* ctx, int32_t* k8_out, float* theta_h_out);
+
 /* LSTM.forward / init_gate_variables (blocks/lstm.py:43-46, 65-88) without a context.
    x [B,T,D]; wx/wh/wy as above; out_a [B,O].  If gates_out is non-NULL it holds six
    [B,T+1,H] tensors that receive i,f,g,o,c,h at t >= 1 (their time-0 slices are the

@@ -456,26 +456,39 @@ def fp64_search(q: str, z, tgt, A, G, rho: float, T: int, kmax: int = 64):
     """The backtracking search of ``admm.py:316-343`` for ONE gate weight, in fp64, from given
     inputs: z [R, H] the pre-activations at W, tgt [R, H] = dual/rho + gate, A [R, K] the rows
     of the side's input (X or H_prev), G [K, H] the (rho-scaled) gradient, i.e. the search
-    direction.  With beta - W = G/theta the test ``f(beta) > est(beta, theta)`` reads
-    ``0.5 rho sum[(phi(z + s A G) - tgt)^2 - (phi(z) - tgt)^2] > (1 + T/2) |G|^2 s``, s = 1/theta
-    (DESIGN.md section 2); the left side is summed as D (2 d0 + D), D = phi(z + s q) - phi(z),
-    without cancellation.  Given the GPU's own z, targets and G this isolates the line-search
-    arithmetic from the fp32 rounding of the state, which moves G itself (the arbiter of
-    ``tests/test_gpu_fullsize.py``).  Returns (k, margin) as ``fp64_decisions``."""
+    direction.  With beta - W = G/theta = s G the test ``f(beta) > est(beta, theta)`` reads
+    f(W + s G) - f(W) > (1 + T/2) |G|^2 s.  G is grad f(W) (admm.py:302-312), so
+    f(W + s G) - f(W) = s |G|^2 + r(s) and the test is r(s) > (T/2) |G|^2 s with the remainder
+    r(s) = 0.5 rho sum[D^2 + 2 d0 (D - s phi'(z) q)], D = phi(z + s q) - phi(z), q = A G,
+    d0 = phi(z) - tgt -- the form the library evaluates (k_select).  In it d0 enters only at
+    second order, so the decision does not depend on the rounding of phi(z) - tgt.
+
+    Returns (k, margin, eps_g): margin = the smallest |r - (T/2)|G|^2 s| / ((T/2)|G|^2 s) of the
+    deciding comparisons (the last failing one and the passing one); eps_g = |G - rho A^T R| / |G|
+    with R = (phi(z) - tgt) phi'(z) in fp64 from the same z and tgt: how much of G itself is the
+    fp32 rounding of the residual (phi(z) - tgt is a difference of O(1) numbers that agree to
+    ~1e-7 when the ADMM residuals are that small) -- recorded, it is the same in the reference."""
     act = torch.tanh if q == 'g' else torch.sigmoid
     z, tgt, A, G = (v.to(torch.float64) for v in (z, tgt, A, G))
     p0 = act(z)
     d0 = p0 - tgt
+    dphi = 1.0 - p0 * p0 if q == 'g' else p0 * (1.0 - p0)
+    g_exact = rho * (A.T @ (d0 * dphi))
+    gn = float(G.norm())
+    # G == 0 exactly (step 1's x side: the stored gates are phi(z) bit for bit): k = 0 is exact
+    eps_g = float((G - g_exact).norm()) / gn if gn > 0 else 0.0
+    del g_exact
     qd = A @ G
-    c = (1.0 + T / 2.0) * float((G * G).sum())
+    lin = dphi * qd
+    c = 0.5 * T * float((G * G).sum())
     tests = []
     for k in range(kmax):
         s = 2.0 ** -k
         D = act(z + qd * s) - p0
-        inc = 0.5 * rho * float((D * (2.0 * d0 + D)).sum())
+        rem = 0.5 * rho * float((D * D + 2.0 * d0 * (D - s * lin)).sum())
         est = c * s
-        tests.append((inc, est))
-        if not inc > est:
+        tests.append((rem, est))
+        if not rem > est:
             break
     ms = [abs(a - b) / b for a, b in tests[-2:] if b > 0]
-    return len(tests) - 1, (min(ms) if ms else float('inf'))
+    return len(tests) - 1, (min(ms) if ms else float('inf')), eps_g

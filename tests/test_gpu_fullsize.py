@@ -36,6 +36,9 @@ from test_gpu_parity import LOSS_RTOL, _loss, _optimizer
 pytestmark = pytest.mark.gpu
 
 W_RTOL = 1e-5
+# decidable searches (eps_g <= 1 %, fp64 margin > 1 %) each trajectory must contain (measured:
+# see DESIGN.md section 2); the step-1 x searches with an exactly zero G count as decidable
+MIN_DECIDABLE = {'c3': 8, 'c5_1gpu': 8, 't2_c2': 4}
 
 
 @pytest.fixture(scope='module')
@@ -74,7 +77,7 @@ def _same_input_fp64(g, opt, pre, gx, gh, model, dev):
         tgt = (L[q][:, 1:, :] / opt.rhos[q].to(dev) + S[q][:, 1:, :]).reshape(B * T, H)   # admm.py:308-309, fp32
         out.append(O.fp64_search(q, zc[qi], tgt, X, gx[qi], rho, T))
         dwx = getattr(model, f'x2{q}').detach().double() - W0[f'x2{q}'].double()
-        zh = zc[qi].double() + X.double() @ dwx
+        zh = (zc[qi].double() + X.double() @ dwx).float()   # the h stage's z, fp32 as the library holds it
         out.append(O.fp64_search(q, zh, tgt, Hp, gh[qi], rho, T))
         del tgt, zh
     return out
@@ -170,7 +173,7 @@ def test_fullsize_matches_reference(name, dev, monkeypatch):
             tie = max(1e-3, 2.0 * r['g_rel_diff'][i])
             assert a == k64 or (margin < tie and abs(a - k64) <= 1), (s, i, r['k'], r['ref_k'], r['fp64'],
                                                                         r['g_rel_diff'])
-    _check_follows_fp64(recs)
+    _check_follows_fp64(recs, MIN_DECIDABLE[name])
     if name == 'c3':   # the trial direction on f32-accurate split3 products: the same run bit for bit
         monkeypatch.setenv('ADMM_Q_PIECES', '3')
         model, opt = _optimizer(g, mods, dev)
@@ -181,19 +184,30 @@ def test_fullsize_matches_reference(name, dev, monkeypatch):
                 assert torch.equal(p.detach(), r['weights'][n]), (r['step'], n)
 
 
-def _check_follows_fp64(recs):
-    """Every GPU exponent equals the fp64 search's from the library's own inputs (z cache,
-    targets, G) wherever that decision's margin exceeds 1 %, whether or
-    not the reference's agrees: the line search itself decides like fp64."""
+EPS_DECIDABLE = 0.01
+
+
+def _check_follows_fp64(recs, min_checked):
+    """The library decides like fp64 wherever the decision is determined by its fp32 inputs.
+
+    Per search, the fp64 search from the library's own inputs (z cache, targets, G) gives k64,
+    its margin, and eps_g, the part of G that is fp32 rounding of the residual (oracle
+    fp64_search).  Where eps_g <= 1 % the search is decidable: k must equal k64 when the margin
+    exceeds 1 % and be within one doubling otherwise.  Where eps_g is larger, G -- in the
+    reference as here -- is dominated by the rounding of phi(z) - tgt and the decision is not
+    reproducible by any fp32 implementation: only within two doublings."""
     checked = 0
     for r in recs:
-        for i, (a, (k64, margin)) in enumerate(zip(r['k'], r['same_input_fp64'])):
-            if margin > 0.01:
+        for i, (a, (k64, margin, eps)) in enumerate(zip(r['k'], r['same_input_fp64'])):
+            if eps <= EPS_DECIDABLE and margin > 0.01:
                 checked += 1
                 assert a == k64, (r['step'], i, r['k'], r['same_input_fp64'])
-            else:
+            elif eps <= EPS_DECIDABLE:
                 assert abs(a - k64) <= 1, (r['step'], i, r['k'], r['same_input_fp64'])
-    assert checked >= 6 * len(recs), checked
+            else:
+                assert abs(a - k64) <= 2, (r['step'], i, r['k'], r['same_input_fp64'])
+    assert checked >= min_checked, (checked, [r['same_input_fp64'] for r in recs])
+    return checked
 
 
 def test_line_search_follows_fp64_c2(dev):
@@ -202,4 +216,74 @@ def test_line_search_follows_fp64_c2(dev):
     g = Golden('t2_c2')
     recs = _run(g, _load_mods(), dev, arbitrate='all')
     _write('t2_c2_fp64', recs, g)
-    _check_follows_fp64(recs)
+    _check_follows_fp64(recs, MIN_DECIDABLE['t2_c2'])
+
+
+def test_c1_forced_replay_all_epochs(dev):
+    """C1 (real GoogleStock windows, hidden 10, 30 epochs as demo.py:337-356) pinned at EVERY epoch.
+
+    From about epoch 15 the reference's fp32 line search decides on rounding noise, so a free
+    run of any other implementation (the reference itself on another CPU included, DESIGN.md
+    section 6) leaves its trajectory there.  Here the library replays the reference's recorded
+    decisions (admm_debug_force: its eight exponents and its h_T search per epoch) while still
+    running every search itself.  Then:
+    * the training AND validation loss of all 30 epochs are within 1e-5 relative of the
+      reference's (the closed forms, GEMMs and sweep agree; only decisions ever differed);
+    * wherever the library's own decision differs from the reference's, it is the fp64 search's
+      from the library's own inputs (z cache, targets, G; exact above a 1 % margin), i.e. the
+      reference departed from fp64, not the library."""
+    from admm_amd import _native as N
+    import ctypes
+    g = Golden('c1_goog')
+    mods = _load_mods()
+    model, opt = _optimizer(g, mods, dev)
+    x, y = g.x.to(dev), g.y.to(dev)
+    vx, vy = g.t('val_x').to(dev), g.t('val_y').to(dev)
+    B, T, H = g.B, g.T, g.H
+    lib = opt._lib
+    gx = torch.zeros(4, g.D, H, device=dev)
+    gh = torch.zeros(4, H, H, device=dev)
+    N.check(lib.admm_debug_trace(opt._ctx, N.ptr(gx), N.ptr(gh)), 'admm_debug_trace')
+    assert _loss(model, vx, vy) == pytest.approx(g.val_losses[0], rel=LOSS_RTOL)
+    departures, recs = 0, []
+    for s in range(1, g.steps + 1):
+        ref_k = g.ks(s)
+        ht_fails = sum(1 for _, _, r in g.searches[s - 1]['hT'] if r)
+        N.check(lib.admm_debug_force(opt._ctx, (ctypes.c_int32 * 8)(*ref_k), ht_fails), 'admm_debug_force')
+        opt._sync_bindings()
+        zc = torch.empty(4, B * T, H, device=dev)
+        assert lib.admm_debug_workspace(opt._ctx, 0, N.ptr(zc), zc.numel() * 4, N.stream_handle(dev)) == 1
+        W0 = {k: p.detach().clone() for k, p in model.named_parameters()}
+        S = {k: v.clone() for k, v in opt.gates.items()}
+        L = {k: v.clone() for k, v in opt.duals.items()}
+        opt.step()
+        own = (ctypes.c_int32 * 8)()
+        th_own = ctypes.c_float()
+        N.check(lib.admm_debug_own(opt._ctx, own, ctypes.byref(th_own)), 'admm_debug_own')
+        own = list(own)
+        assert list(opt.last_step_stats()['k'].values()) == ref_k
+        tr, va = _loss(model, x, y), _loss(model, vx, vy)
+        recs.append({'epoch': s, 'train': tr, 'ref_train': g.losses[s], 'val': va, 'ref_val': g.val_losses[s],
+                     'ref_k': ref_k, 'own_k': own, 'theta_h_own': th_own.value})
+        assert tr == pytest.approx(g.losses[s], rel=LOSS_RTOL), (s, tr, g.losses[s])
+        assert va == pytest.approx(g.val_losses[s], rel=LOSS_RTOL), (s, va, g.val_losses[s])
+        if own != ref_k:
+            departures += 1
+            same = _same_input_fp64(g, opt, (zc, W0, S, L), gx, gh, model, dev)
+            recs[-1]['same_input_fp64'] = same
+            for i, (a, r) in enumerate(zip(own, ref_k)):
+                if a == r:
+                    continue
+                k64, margin, eps = same[i]
+                if a < 0:      # the library's first window did not decide: fp64 must be beyond it too
+                    assert k64 >= 16, (s, i, own, ref_k, same)
+                elif eps <= EPS_DECIDABLE and margin > 0.01:
+                    assert a == k64, (s, i, own, ref_k, same)
+                elif eps <= EPS_DECIDABLE:
+                    assert abs(a - k64) <= 1, (s, i, own, ref_k, same)
+    N.check(lib.admm_debug_force(opt._ctx, None, 0), 'admm_debug_force')
+    out = os.environ.get('ADMM_PARITY_OUT')
+    if out:
+        os.makedirs(out, exist_ok=True)
+        with open(os.path.join(out, 'parity_c1_forced.json'), 'w') as f:
+            json.dump({'departures': departures, 'epochs': recs}, f, indent=1)

@@ -225,8 +225,11 @@ def test_line_search_matches_fp64_oracle(shape, variant, mods, dev):
 @pytest.mark.parametrize('pair', [0, 2])
 @pytest.mark.parametrize('tanh_gate', [0, 1])
 def test_trial_increments_vs_fp64(tanh_gate, pair, dev):
-    """The trial-pass arithmetic: sum_e [(phi(z+q 2^-k)-t)^2 - (phi(z)-t)^2] vs numpy fp64, for the
-    generic kernels' per-element form and (pair = 2) the fast kernels' packed pair form."""
+    """The trial-pass arithmetic vs numpy fp64, for the generic kernels' per-element form and
+    (pair = 2) the fast kernels' packed pair form: the remainder past the first-order term,
+    sum_e [D^2 + 2 d0 (D - s phi'(z) q)], D = phi(z + q s) - phi(z), d0 = phi(z) - t, s = 2^-k
+    (k_select compares it with (T/2) |G|^2 s).  The per-candidate elements form it as their whole
+    increment minus the first-order term, so the bound scales with both."""
     from admm_amd import _native as N
     lib = N.load()
     rng = np.random.default_rng(5)
@@ -239,16 +242,19 @@ def test_trial_increments_vs_fp64(tanh_gate, pair, dev):
     zt, tt, qt = (torch.from_numpy(a).to(dev) for a in (z, tgt, q))
     z64, t64, q64 = z.astype(np.float64), tgt.astype(np.float64), q.astype(np.float64)
     d0 = phi(z64) - t64
+    lin = (1 - np.tanh(z64) ** 2 if tanh_gate else phi(z64) * (1 - phi(z64))) * q64
     for kbase in (0, 16):
         out = (ctypes.c_double * 16)()
         N.check(lib.admm_debug_trial(N.ptr(zt), N.ptr(tt), N.ptr(qt), n, tanh_gate | pair, kbase, out,
                                      N.stream_handle(dev)), 'admm_debug_trial')
         for k in range(16):
             kk = kbase + k
-            d1 = phi(z64 + q64 * 2.0 ** -kk) - t64
-            inc = (d1 - d0) * (d1 + d0)
-            ref = inc.sum()
-            scale = np.abs(inc).sum()
+            sk = 2.0 ** -kk
+            d1 = phi(z64 + q64 * sk) - t64
+            # the remainder past the first-order term (k_select): D^2 + 2 d0 (D - s phi' q)
+            rem = (d1 - d0) ** 2 + 2 * d0 * ((d1 - d0) - sk * lin)
+            ref = rem.sum()
+            scale = np.abs(rem).sum() + np.abs(2 * d0 * sk * lin).sum()
             assert abs(out[k] - ref) <= 2e-5 * scale + 1e-30, (kk, out[k], ref, scale)
 
 
@@ -256,7 +262,8 @@ def test_trial_increments_vs_fp64(tanh_gate, pair, dev):
 @pytest.mark.parametrize('tanh_gate', [0, 1])
 def test_trial_polynomial_band_vs_fp64(tanh_gate, pair, dev):
     """Elements at the top of the polynomial regime (|q| in [2^-9, 2^-5]: 5-term Taylor in s,
-    admm_kernels.hpp kPolyQ), every exponent of the first two windows, vs numpy fp64."""
+    admm_kernels.hpp kPolyQ), every exponent of the first two windows, vs numpy fp64 (the
+    remainder past the first-order term, as test_trial_increments_vs_fp64)."""
     from admm_amd import _native as N
     lib = N.load()
     rng = np.random.default_rng(6)
@@ -268,15 +275,17 @@ def test_trial_polynomial_band_vs_fp64(tanh_gate, pair, dev):
     zt, tt, qt = (torch.from_numpy(a).to(dev) for a in (z, tgt, q))
     z64, t64, q64 = z.astype(np.float64), tgt.astype(np.float64), q.astype(np.float64)
     d0 = phi(z64) - t64
+    lin = (1 - np.tanh(z64) ** 2 if tanh_gate else phi(z64) * (1 - phi(z64))) * q64
     for kbase in (0, 16):
         out = (ctypes.c_double * 16)()
         N.check(lib.admm_debug_trial(N.ptr(zt), N.ptr(tt), N.ptr(qt), n, tanh_gate | pair, kbase, out,
                                      N.stream_handle(dev)), 'admm_debug_trial')
         for k in range(16):
             kk = kbase + k
-            d1 = phi(z64 + q64 * 2.0 ** -kk) - t64
-            inc = (d1 - d0) * (d1 + d0)
-            ref, scale = inc.sum(), np.abs(inc).sum()
+            sk = 2.0 ** -kk
+            d1 = phi(z64 + q64 * sk) - t64
+            rem = (d1 - d0) ** 2 + 2 * d0 * ((d1 - d0) - sk * lin)   # the remainder (k_select)
+            ref, scale = rem.sum(), np.abs(rem).sum()
             assert abs(out[k] - ref) <= 2e-6 * scale + 1e-30, (kk, out[k], ref, scale)
 
 

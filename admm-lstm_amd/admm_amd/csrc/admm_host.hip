@@ -119,10 +119,12 @@ struct AdmmCtx {
   bool sweep_rows = false; // whole sweep as one persistent launch (k_sweep_rows; ADMM_SWEEP_ROWS=0 disables)
   float* swt = nullptr;    // its B-operand image of the weights
   bool split3 = false;     // h-stage GEMMs on split bf16 MFMAs (admm_split3.hip; ADMM_SPLIT3=0 disables)
-  // split pieces of the trial direction GEMM Q = Hprev G (ADMM_Q_PIECES=3: f32-accurate).  Q only
-  // enters the line-search increments, where 2^-16 relative is far inside the reference's own
-  // rounding of W + G/theta (DESIGN.md "trial direction precision"); G itself stays split3.
-  int q_pieces = 2;
+  // pieces of the trial direction GEMM Q = Hprev G: 1 = Hprev in two bf16 pieces, G in one (G
+  // rounded to bf16, ~2^-9 relative per element: the line-search remainder moves by ~0.4 %, against
+  // decision margins of >= 12 % on the h side at C3 and C5); 2 = two-piece G (~2^-16); 3 = split3,
+  // f32-accurate (ADMM_Q_PIECES).  Q only enters the line-search increments (DESIGN.md "trial
+  // direction precision"); G itself, which updates the weights, is not rounded.
+  int q_pieces = 1;
   // split pieces of the h-side gradient G_h = rho Hprev^T R (k_atr3w): 2 = the three products of
   // two-way splits, ~2^-16 relative per product -- the accuracy of the reference's own fp32 sums of
   // B*T terms (DESIGN.md "h-side gradient on two-way splits"); ADMM_ATR_PIECES=3: f32-accurate split3

@@ -36,9 +36,6 @@ from test_gpu_parity import LOSS_RTOL, _loss, _optimizer
 pytestmark = pytest.mark.gpu
 
 W_RTOL = 1e-5
-# decidable searches (eps_g <= 1 %, fp64 margin > 1 %) each trajectory must contain (measured:
-# see DESIGN.md section 2); the step-1 x searches with an exactly zero G count as decidable
-MIN_DECIDABLE = {'c3': 8, 'c5_1gpu': 8, 't2_c2': 4}
 
 
 @pytest.fixture(scope='module')
@@ -173,7 +170,7 @@ def test_fullsize_matches_reference(name, dev, monkeypatch):
             tie = max(1e-3, 2.0 * r['g_rel_diff'][i])
             assert a == k64 or (margin < tie and abs(a - k64) <= 1), (s, i, r['k'], r['ref_k'], r['fp64'],
                                                                         r['g_rel_diff'])
-    _check_follows_fp64(recs, MIN_DECIDABLE[name])
+    _check_follows_fp64(recs)
     if name == 'c3':   # the trial direction on f32-accurate split3 products: the same run bit for bit
         monkeypatch.setenv('ADMM_Q_PIECES', '3')
         model, opt = _optimizer(g, mods, dev)
@@ -184,29 +181,24 @@ def test_fullsize_matches_reference(name, dev, monkeypatch):
                 assert torch.equal(p.detach(), r['weights'][n]), (r['step'], n)
 
 
-EPS_DECIDABLE = 0.01
+def _check_follows_fp64(recs):
+    """The library decides like fp64 from its own inputs.
 
-
-def _check_follows_fp64(recs, min_checked):
-    """The library decides like fp64 wherever the decision is determined by its fp32 inputs.
-
-    Per search, the fp64 search from the library's own inputs (z cache, targets, G) gives k64,
-    its margin, and eps_g, the part of G that is fp32 rounding of the residual (oracle
-    fp64_search).  Where eps_g <= 1 % the search is decidable: k must equal k64 when the margin
-    exceeds 1 % and be within one doubling otherwise.  Where eps_g is larger, G -- in the
-    reference as here -- is dominated by the rounding of phi(z) - tgt and the decision is not
-    reproducible by any fp32 implementation: only within two doublings."""
+    Per search, the fp64 search from the library's z cache, targets and G (oracle fp64_search)
+    gives k64 and its margin: k must equal k64 where the margin exceeds 1 %, and be within one
+    doubling below that.  Both evaluate the reference's test as the remainder past the
+    first-order term (k_select), which does not depend on the rounding of phi(z) - tgt; eps_g
+    (recorded) is how much of G itself is that rounding -- large at C3 and C1, in the reference
+    as here.  Nearly every search must be a checked one."""
     checked = 0
     for r in recs:
-        for i, (a, (k64, margin, eps)) in enumerate(zip(r['k'], r['same_input_fp64'])):
-            if eps <= EPS_DECIDABLE and margin > 0.01:
+        for i, (a, (k64, margin, _eps)) in enumerate(zip(r['k'], r['same_input_fp64'])):
+            if margin > 0.01:
                 checked += 1
                 assert a == k64, (r['step'], i, r['k'], r['same_input_fp64'])
-            elif eps <= EPS_DECIDABLE:
-                assert abs(a - k64) <= 1, (r['step'], i, r['k'], r['same_input_fp64'])
             else:
-                assert abs(a - k64) <= 2, (r['step'], i, r['k'], r['same_input_fp64'])
-    assert checked >= min_checked, (checked, [r['same_input_fp64'] for r in recs])
+                assert abs(a - k64) <= 1, (r['step'], i, r['k'], r['same_input_fp64'])
+    assert checked >= 6 * len(recs), (checked, [r['same_input_fp64'] for r in recs])
     return checked
 
 
@@ -216,7 +208,7 @@ def test_line_search_follows_fp64_c2(dev):
     g = Golden('t2_c2')
     recs = _run(g, _load_mods(), dev, arbitrate='all')
     _write('t2_c2_fp64', recs, g)
-    _check_follows_fp64(recs, MIN_DECIDABLE['t2_c2'])
+    _check_follows_fp64(recs)
 
 
 def test_c1_forced_replay_all_epochs(dev):
@@ -274,12 +266,12 @@ def test_c1_forced_replay_all_epochs(dev):
             for i, (a, r) in enumerate(zip(own, ref_k)):
                 if a == r:
                     continue
-                k64, margin, eps = same[i]
+                k64, margin, _eps = same[i]
                 if a < 0:      # the library's first window did not decide: fp64 must be beyond it too
                     assert k64 >= 16, (s, i, own, ref_k, same)
-                elif eps <= EPS_DECIDABLE and margin > 0.01:
+                elif margin > 0.01:
                     assert a == k64, (s, i, own, ref_k, same)
-                elif eps <= EPS_DECIDABLE:
+                else:
                     assert abs(a - k64) <= 1, (s, i, own, ref_k, same)
     N.check(lib.admm_debug_force(opt._ctx, None, 0), 'admm_debug_force')
     out = os.environ.get('ADMM_PARITY_OUT')

@@ -129,9 +129,10 @@ struct AdmmCtx {
   // two-way splits, ~2^-16 relative per product -- the accuracy of the reference's own fp32 sums of
   // B*T terms (DESIGN.md "h-side gradient on two-way splits"); ADMM_ATR_PIECES=3: f32-accurate split3
   int atr_pieces = 2;
-  bool atr3w = true;
-  // Q in the row-quad layout (k_qgemm3 -> k_trial_rows<1>; ADMM_QPAIR=0: row-major)
-  bool qpair = true;       // k_atr3w (two waves per SIMD) for the h-side gradient; ADMM_ATR3W=0: k_atr3
+  bool atr3w = true;       // k_atr3w (two waves per SIMD) for the h-side gradient; ADMM_ATR3W=0: k_atr3
+  // Q in the row-quad layout (k_qgemm3 -> k_trial_rows<1>): 2 = bf16 elements (default), 1 = f32,
+  // 0 = row-major f32 (ADMM_QPAIR)
+  int qpair = 2;
   float* gimg = nullptr;   // split image of G_h for k_qgemm3
   hipStream_t sx[kMaxSweepStreams - 1] = {};
   hipEvent_t ev_fork = nullptr, ev_join[kMaxSweepStreams - 1] = {};
@@ -353,7 +354,7 @@ int stage_weights(AdmmCtx* c, int side, hipStream_t s) {
       if (fast)
         launch_trial_fast(g, side, pass, side == 1 ? zh : c->zc, c->tgt, side == 1 ? c->Q : nullptr, c->buf.x,
                           side == 0 ? c->G : c->dW, c->found + 4 * (pass & 1), c->tr_part, nblk, s, sx.zx ? &sx : nullptr,
-                          side == 1 && c->split3 && c->qpair);
+                          side == 1 && c->split3 ? c->qpair : 0);
       else
         launch_trial(g, pass, c->zc, c->tgt, c->Q, c->found + 4 * (pass & 1), c->tr_part, nblk, s);
     }
@@ -499,7 +500,7 @@ int admm_create(const AdmmDims* dims, const AdmmParams* params, int device, Admm
   if (const char* e = std::getenv("ADMM_SPEC_X")) c->spec_x = c->spec_x && std::atoi(e) != 0;
   if (const char* e = std::getenv("ADMM_SPLIT3")) c->split3 = c->split3 && std::atoi(e) != 0;
   if (const char* e = std::getenv("ADMM_ATR3W")) c->atr3w = std::atoi(e) != 0;
-  if (const char* e = std::getenv("ADMM_QPAIR")) c->qpair = std::atoi(e) != 0;
+  if (const char* e = std::getenv("ADMM_QPAIR")) c->qpair = std::max(0, std::min(2, std::atoi(e)));
   if (const char* e = std::getenv("ADMM_Q_PIECES")) c->q_pieces = std::max(1, std::min(3, std::atoi(e)));
   if (const char* e = std::getenv("ADMM_ATR_PIECES")) c->atr_pieces = std::atoi(e) == 2 ? 2 : 3;
   Hyper& h = c->hp;

@@ -1631,7 +1631,7 @@ __global__ __launch_bounds__(kThreads, TF_MINB) void k_trial_fast(Geom g, int pa
 // halves of trial_pair's packed arithmetic; the next pair's operands are loaded while this one
 // is evaluated.  Side 1 reads q from Q instead and walks row quads (QP: Q in k_qgemm3's
 // row-quad layout [row / 4][j][row % 4], one float4 per quad).
-template <bool TANH, int SIDE, int DP, bool XV, bool SPEC, bool QP = false>
+template <bool TANH, int SIDE, int DP, bool XV, bool SPEC, int QP = 0>
 __device__ __forceinline__ void trial_rows_body(const Geom& g, int q, int pass, const float* __restrict__ zc,
                                                 const float* __restrict__ tgt, const float* __restrict__ Q,
                                                 const float* __restrict__ x, const float* __restrict__ Gx, int blk,
@@ -1679,7 +1679,14 @@ __device__ __forceinline__ void trial_rows_body(const Geom& g, int q, int pass, 
         v.z[h] = f32x2{__builtin_nontemporal_load(zq + r[2 * h] * g.H), __builtin_nontemporal_load(zq + r[2 * h + 1] * g.H)};
         v.t[h] = f32x2{__builtin_nontemporal_load(tq + r[2 * h] * g.H), __builtin_nontemporal_load(tq + r[2 * h + 1] * g.H)};
       }
-      if constexpr (QP) {   // BT % 4 == 0: one quad
+      if constexpr (QP == 2) {   // bf16 quads: 8 B per row quad and column
+        const int64_t pr = __builtin_amdgcn_readfirstlane((int)((ra < BT ? ra : BT - 4) >> 2));
+        const __bf16* Qb = reinterpret_cast<const __bf16*>(Q) + (int64_t)q * n + 4 * j;
+        const f32x4 qq = __builtin_convertvector(
+            __builtin_nontemporal_load(reinterpret_cast<const bf16x4*>(Qb + pr * 4 * g.H)), f32x4);
+        v.q[0] = f32x2{qq[0], qq[1]};
+        v.q[1] = f32x2{qq[2], qq[3]};
+      } else if constexpr (QP == 1) {   // BT % 4 == 0: one quad
         const int64_t pr = __builtin_amdgcn_readfirstlane((int)((ra < BT ? ra : BT - 4) >> 2));
         const f32x4 qq = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(Qq + pr * 4 * g.H));
         v.q[0] = f32x2{qq[0], qq[1]};
@@ -1773,7 +1780,7 @@ __device__ __forceinline__ void trial_rows_body(const Geom& g, int q, int pass, 
   dq_run<TANH>(dq, acc, true);
 }
 
-template <int SIDE, int DP, bool XV, bool SPEC, bool QP = false>
+template <int SIDE, int DP, bool XV, bool SPEC, int QP = 0>
 __global__ __launch_bounds__(kThreads) void k_trial_rows(Geom g, int pass, const float* __restrict__ zc,
                                                          const float* __restrict__ tgt, const float* __restrict__ Q,
                                                          const float* __restrict__ x, const float* __restrict__ Gx,
@@ -2899,13 +2906,15 @@ bool trial_mx_ok(const Geom& g) {   // ADMM_TRIAL_MX=0: the x side on k_trial_ro
 
 void launch_trial_fast(const Geom& g, int side, int pass, const float* zc, const float* tgt, const float* Q,
                        const float* x, const float* Wsrc, const int* found, double* part, int nblk, hipStream_t s,
-                       const SpecX* spec, bool qpair) {
+                       const SpecX* spec, int qpair) {
   dim3 grid(nblk, 4);
   const SpecX sp = spec ? *spec : SpecX{};
   if (side == 1 && trial_rows_ok(g)) {
     dim3 gr(nblk, 4, g.H / 256);
-    if (qpair && qpair_ok(g))
-      k_trial_rows<1, 4, false, false, true><<<gr, kThreads, 0, s>>>(g, pass, zc, tgt, Q, x, Wsrc, found, part, nblk, sp);
+    if (qpair == 2 && qpair_ok(g))
+      k_trial_rows<1, 4, false, false, 2><<<gr, kThreads, 0, s>>>(g, pass, zc, tgt, Q, x, Wsrc, found, part, nblk, sp);
+    else if (qpair == 1 && qpair_ok(g))
+      k_trial_rows<1, 4, false, false, 1><<<gr, kThreads, 0, s>>>(g, pass, zc, tgt, Q, x, Wsrc, found, part, nblk, sp);
     else
       k_trial_rows<1, 4, false, false><<<gr, kThreads, 0, s>>>(g, pass, zc, tgt, Q, x, Wsrc, found, part, nblk, sp);
     return;

@@ -182,7 +182,7 @@ struct SpecX {
 };
 void launch_trial_fast(const Geom& g, int side, int pass, const float* zc, const float* tgt, const float* Q,
                        const float* x, const float* Wsrc, const int* found, double* part, int nblk, hipStream_t s,
-                       const SpecX* spec = nullptr, bool qpair = false);
+                       const SpecX* spec = nullptr, int qpair = 0);
 // after the x decision: zx = zc + X dWx for the gates whose exponent was mispredicted
 void launch_apply_fix(const Geom& g, const float* x, const float* dW, const float* zc, float* zx, const int* kpred,
                       const DevStats* stats, hipStream_t s);
@@ -213,14 +213,15 @@ void launch_atr3(const Geom& g, const float* Sh, const float* zc, const float* t
 // pieces = 3: f32-accurate split3 products; 2: two-way splits, three products (~2^-16 relative),
 // enough for the trial direction ("trial direction precision")
 // qpair (and qpair_ok: BT % 4 == 0): Q in the row-quad layout [q][row / 4][j][row % 4] that
-// launch_trial_fast(..., qpair = true) reads (the h-side trial pass, H % 256 == 0)
+// launch_trial_fast(..., qpair) reads (the h-side trial pass, H % 256 == 0); 1 = f32, 2 = bf16
+// elements (0: row-major f32)
 bool qpair_ok(const Geom& g);
 void launch_qgemm3(const Geom& g, const float* Sh, const float* G, float* gimg, float* Q, hipStream_t s,
-                   int pieces = 3, bool qpair = false);
+                   int pieces = 3, int qpair = 0);
 // the two halves of launch_qgemm3: G -> split image, then Q = Hprev G (gates with found[q] set skipped)
 void launch_split_g(const Geom& g, const float* G, float* gimg, hipStream_t s);
 void launch_qgemm3_img(const Geom& g, const float* Sh, const float* gimg, float* Q, const int* found, hipStream_t s,
-                       int pieces = 3, bool qpair = false);
+                       int pieces = 3, int qpair = 0);
 // decide the first passing k in this pass's window; on success update the weights
 struct SelectArgs {
   int side;                 // 0 x, 1 h

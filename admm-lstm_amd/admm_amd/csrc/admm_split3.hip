@@ -21,6 +21,8 @@
 // halves) are then conflict-free under the gfx950 bank rules (MI355X_MICROARCH.md §LDS).
 #include "admm_split3.hpp"
 
+#include <type_traits>
+
 namespace admm {
 namespace {
 
@@ -54,7 +56,11 @@ __global__ __launch_bounds__(kThreads) void k_split_g(int H, const float* __rest
 // stores 16 B and a wave-instruction two contiguous 512-B runs -- a quarter of the store
 // instructions of the row-major layout (the epilogue is store-issue bound); the h-side trial
 // reads a row pair (rows 2i, 2i + 1: one half of a quad) as one float2.
-template <int NP, bool QP, int BM>
+// QP = 2: the same row-quad layout in bf16 (Q[q][row / 4][j][row % 4] as bf16x4, 8 B per quad and
+// column): Q only enters the line-search remainder, where its ~2^-9 relative rounding moves the
+// decision quantity by ~2^-8 (DESIGN.md "trial direction precision"); half the bytes written here
+// and read back by the h-side trials.
+template <int NP, int QP, int BM>
 __global__ __launch_bounds__(2 * BM) void k_qgemm3(Geom g, const float* __restrict__ Sh,
                                                     const bf16x8* __restrict__ gi, float* __restrict__ Q,
                                                     const int* __restrict__ found) {
@@ -70,7 +76,23 @@ __global__ __launch_bounds__(2 * BM) void k_qgemm3(Geom g, const float* __restri
   qgemm3_tile<NP, BM>(g, Sh, gi, q, cb, m0, lds, acc);
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, wr = wave >> 1, wc = wave & 1, c32 = lane & 31;
   float* Qq = Q + (int64_t)q * BT * H + Q3_BN * cb + wc * 128 + c32;
-  if constexpr (QP) {
+  if constexpr (QP == 2) {
+    bf16x4* Qp = reinterpret_cast<bf16x4*>(reinterpret_cast<__bf16*>(Q) + (int64_t)q * BT * H) + Q3_BN * cb + wc * 128 + c32;
+#pragma unroll
+    for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+      for (int r = 0; r < 16; r += 4) {
+        const int64_t row = m0 + wr * 64 + mi * 32 + acc_row(r, lane);   // a multiple of 4
+        if (row >= BT) continue;
+#pragma unroll
+        for (int ni = 0; ni < 4; ++ni) {
+          const f32x4 v = f32x4{acc[mi][ni][r], acc[mi][ni][r + 1], acc[mi][ni][r + 2], acc[mi][ni][r + 3]};
+          __builtin_nontemporal_store(__builtin_convertvector(v, bf16x4), Qp + (row >> 2) * H + ni * 32);
+        }
+      }
+    return;
+  }
+  if constexpr (QP == 1) {
     f32x4* Qp = reinterpret_cast<f32x4*>(Q + (int64_t)q * BT * H) + Q3_BN * cb + wc * 128 + c32;
 #pragma unroll
     for (int mi = 0; mi < 2; ++mi)
@@ -514,7 +536,7 @@ void launch_split_g(const Geom& g, const float* G, float* gimg, hipStream_t s) {
 bool qpair_ok(const Geom& g) { return g.BT() % 4 == 0; }
 
 void launch_qgemm3_img(const Geom& g, const float* Sh, const float* gimg, float* Q, const int* found, hipStream_t s,
-                       int pieces, bool qpair) {
+                       int pieces, int qpair) {
   // 128-row tiles, two workgroups per CU.  Q3_BM2=256 (8 waves, half the G-image reads per Q row)
   // measured slower at C3: 0.54 against 0.48 ms -- the two independent workgroups of a CU drift
   // out of phase, one staging while the other multiplies, where one workgroup's barriers keep
@@ -523,20 +545,23 @@ void launch_qgemm3_img(const Geom& g, const float* Sh, const float* gimg, float*
 #define Q3_BM2 128
 #endif
   const bf16x8* gb = reinterpret_cast<const bf16x8*>(gimg);
-  qpair = qpair && qpair_ok(g);
+  const int qp = qpair_ok(g) ? qpair : 0;
   const int BM = pieces == 2 ? Q3_BM2 : 128;   // (pieces 1: 128)
   const int64_t nrt = (g.BT() + BM - 1) / BM;
   dim3 grid((unsigned)(nrt * 4 * (g.H / Q3_BN)));
-  if (pieces == 1 && qpair) k_qgemm3<1, true, 128><<<grid, 256, 0, s>>>(g, Sh, gb, Q, found);
-  else if (pieces == 1) k_qgemm3<1, false, 128><<<grid, 256, 0, s>>>(g, Sh, gb, Q, found);
-  else if (pieces == 2 && qpair) k_qgemm3<2, true, Q3_BM2><<<grid, 2 * Q3_BM2, 0, s>>>(g, Sh, gb, Q, found);
-  else if (pieces == 2) k_qgemm3<2, false, Q3_BM2><<<grid, 2 * Q3_BM2, 0, s>>>(g, Sh, gb, Q, found);
-  else if (qpair) k_qgemm3<3, true, 128><<<grid, 256, 0, s>>>(g, Sh, gb, Q, found);
-  else k_qgemm3<3, false, 128><<<grid, 256, 0, s>>>(g, Sh, gb, Q, found);
+  auto go = [&](auto qpm) {
+    constexpr int QPM = decltype(qpm)::value;
+    if (pieces == 1) k_qgemm3<1, QPM, 128><<<grid, 256, 0, s>>>(g, Sh, gb, Q, found);
+    else if (pieces == 2) k_qgemm3<2, QPM, Q3_BM2><<<grid, 2 * Q3_BM2, 0, s>>>(g, Sh, gb, Q, found);
+    else k_qgemm3<3, QPM, 128><<<grid, 256, 0, s>>>(g, Sh, gb, Q, found);
+  };
+  if (qp == 2) go(std::integral_constant<int, 2>{});
+  else if (qp == 1) go(std::integral_constant<int, 1>{});
+  else go(std::integral_constant<int, 0>{});
 }
 
 void launch_qgemm3(const Geom& g, const float* Sh, const float* G, float* gimg, float* Q, hipStream_t s, int pieces,
-                   bool qpair) {
+                   int qpair) {
   launch_split_g(g, G, gimg, s);
   launch_qgemm3_img(g, Sh, gimg, Q, nullptr, s, pieces, qpair);
 }

@@ -862,6 +862,37 @@ def test_q_two_piece_split_same_trajectory(shape, pieces, mods, dev, monkeypatch
     assert torch.equal(out[0][1], out[1][1])
 
 
+@pytest.mark.parametrize('shape', [(1000, 5, 16, 256), (300, 4, 1, 512)])
+def test_q_bf16_storage_same_trajectory(shape, mods, dev, monkeypatch):
+    """Q stored in bf16 (ADMM_QPAIR=2, the default) against f32 (ADMM_QPAIR=1), the same row-quad
+    layout: Q only enters the line-search remainder, so with the same exponents the trajectories
+    are bitwise equal -- every exponent of several steps must agree."""
+    from blocks.lstm import LSTM
+    from parameters import example_parameter_dictionary
+    admm, nd = mods
+    admm.with_dual_y = False
+    B, T, D, H = shape
+    g = torch.Generator().manual_seed(31)
+    x = torch.rand(B, T, D, generator=g).to(dev)
+    y = (0.8 * x.mean((1, 2)).unsqueeze(1) + 0.1 * torch.rand(B, 1, generator=g).to(dev)).contiguous()
+    mod = admm if H == 256 else nd
+    out = []
+    for mode in ('1', '2'):
+        monkeypatch.setenv('ADMM_QPAIR', mode)
+        torch.manual_seed(0)
+        m = LSTM(D, H, 1).to(dev)
+        opt = mod.ADMMBasedOptimizer(m, (x, y), example_parameter_dictionary['GoogleStock'], verbose=False)
+        ks = []
+        for _ in range(5):
+            opt.step()
+            ks.append(list(opt.last_step_stats()['k'].values()))
+        out.append((ks, torch.cat([p.detach().flatten() for p in m.parameters()]
+                                  + [v.flatten() for v in opt.gates.values()])))
+        del opt
+    assert out[0][0] == out[1][0]
+    assert torch.equal(out[0][1], out[1][1])
+
+
 @pytest.mark.parametrize('shape', [(2048, 8, 16, 256), (300, 3, 16, 512)])
 def test_atr_two_piece_split_same_decisions(shape, mods, dev, monkeypatch):
     """The h-side gradient G_h = rho Hprev^T R on two-way bf16 splits (three products, the

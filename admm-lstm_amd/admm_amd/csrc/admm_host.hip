@@ -129,6 +129,9 @@ struct AdmmCtx {
   // two-way splits, ~2^-16 relative per product -- the accuracy of the reference's own fp32 sums of
   // B*T terms (DESIGN.md "h-side gradient on two-way splits"); ADMM_ATR_PIECES=3: f32-accurate split3
   int atr_pieces = 2;
+  // pass 0 of a gate whose last exponent was past the first window also sums the per-candidate
+  // elements' polynomial, so the exponents past it are decided without pass 1 (ADMM_P16=0: off)
+  bool p16 = true;
   bool atr3w = true;       // k_atr3w (two waves per SIMD) for the h-side gradient; ADMM_ATR3W=0: k_atr3
   // Q in the row-quad layout (k_qgemm3 -> k_trial_rows<1>): 2 = bf16 elements (default), 1 = f32,
   // 0 = row-major f32 (ADMM_QPAIR)
@@ -313,7 +316,8 @@ int stage_weights(AdmmCtx* c, int side, hipStream_t s) {
     ProfScope ps(c, side == 0 ? ADMM_PROF_ATR_X : ADMM_PROF_ATR_H, s);
     launch_atr(g, side, c->buf.x, c->buf.gates[ADMM_H], c->R, c->gslab, ns, s);
   }
-  launch_reduce_g(g, side, c->hp, gsrc, ns, c->G, c->found, spec && side == 0 ? c->kpred : nullptr, c->stats, s);
+  launch_reduce_g(g, side, c->hp, gsrc, ns, c->G, c->found, spec && side == 0 ? c->kpred : nullptr, c->stats, s,
+                  c->p16);
   int rc = allreduce_f32(c, c->G, (size_t)4 * Kd * g.H, s);
   if (rc) return rc;
   if (c->trace_g[side])
@@ -503,6 +507,7 @@ int admm_create(const AdmmDims* dims, const AdmmParams* params, int device, Admm
   if (const char* e = std::getenv("ADMM_QPAIR")) c->qpair = std::max(0, std::min(2, std::atoi(e)));
   if (const char* e = std::getenv("ADMM_Q_PIECES")) c->q_pieces = std::max(1, std::min(3, std::atoi(e)));
   if (const char* e = std::getenv("ADMM_ATR_PIECES")) c->atr_pieces = std::atoi(e) == 2 ? 2 : 3;
+  if (const char* e = std::getenv("ADMM_P16")) c->p16 = std::atoi(e) != 0;
   Hyper& h = c->hp;
   for (int i = 0; i < 7; ++i) h.rho[i] = params->rho[i];
   h.rinv_exact = 1;
@@ -541,7 +546,7 @@ int admm_create(const AdmmDims* dims, const AdmmParams* params, int device, Admm
       (rc = dalloc(&c->gslab, slab)) ||
       (rc = dalloc(&c->tr_part, (size_t)4 * kTrialSlots * c->nblk_trial)) ||
       (rc = dalloc(&c->tr_sums, (size_t)4 * kTrialSlots)) || (rc = dalloc(&c->tr_poly, (size_t)4 * kPolyN)) ||
-      (rc = dalloc(&c->found, 8)) || (rc = dalloc(&c->pick, 4)) ||
+      (rc = dalloc(&c->found, 12)) || (rc = dalloc(&c->pick, 4)) ||
       (rc = dalloc(&c->U, (size_t)g.B * g.O)) || (rc = dalloc(&c->wy_slab, (size_t)c->wy_nsplit * g.H * g.O)) ||
       (rc = dalloc(&c->Gy, (size_t)g.H * g.O)) || (rc = dalloc(&c->ht_part, (size_t)c->ht_nblk * kHTSums)) ||
       (rc = dalloc(&c->ht_sums, kHTSums)) || (rc = dalloc(&c->stats, 1)) || (rc = dalloc(&c->lamh_nz, 1)) || (rc = dalloc(&c->force_dev, 9)) ||

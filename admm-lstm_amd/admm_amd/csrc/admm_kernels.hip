@@ -1018,13 +1018,17 @@ __global__ __launch_bounds__(kThreads) void k_atr_fused(Geom g, const float* x, 
     atr_fused_body<BM, WM, KC, false>(g, x, Sh, zc, tgt, dW, slab, nsplit, smem);
 }
 
-__global__ __launch_bounds__(kThreads) void k_reduce_g(int Kd, int H, Hyper hp, const float* slab, int nsplit,
-                                                         float* G, int* found, int* kpred, const DevStats* stats) {
+__global__ __launch_bounds__(kThreads) void k_reduce_g(int Kd, int H, int side, int p16, Hyper hp, const float* slab,
+                                                         int nsplit, float* G, int* found, int* kpred,
+                                                         const DevStats* stats) {
   const int64_t per_q = (int64_t)Kd * H;
   const int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x;
   if (i < 4) {
     found[i] = 0;   // this stage's line searches start undecided (no memset launch)
     if (kpred) kpred[i] = stats->k[2 * i];   // last step's x-side exponent (SpecX)
+    // hint: the gate's last exponent on this side was past pass 0's window, so pass 0 also forms
+    // the per-candidate elements' polynomial for k >= kTrialJ (dq_hint, k_select)
+    found[8 + i] = p16 && stats->k[2 * i + side] >= kTrialJ ? 1 : 0;
   }
   if (i >= 4 * per_q) return;
   const int q = (int)(i / per_q);
@@ -1129,15 +1133,77 @@ __global__ __launch_bounds__(kThreads) void k_qgemm(Geom g, const float* x, cons
 // Slot layout per gate: kSlots = [J candidates][6 poly][sum d0^2][#per-candidate elements].
 constexpr int kSlots = kTrialSlots;
 constexpr int kSlotPoly = kTrialJ, kSlotFw = kTrialJ + kPolyN, kSlotNne = kTrialJ + kPolyN + 1;
+constexpr int kSlotP16 = kSlotNne + 1, kSlotN16 = kSlotP16 + kPolyHiN;
+
+// Per-wave queue of the elements in the per-candidate regime.  Which elements need the
+// 16-candidate loop is data dependent (on C3, 0-95 % per gate), so evaluating it in place
+// would run the loop for the whole wave whenever any lane needs it.  Instead each element's
+// five inputs are appended (ballot + prefix count) to an LDS ring of this wave, and the
+// loop runs once 64 entries are pending, with every lane busy.  All lanes of a wave must
+// make the same sequence of dq_push / dq_run calls (loops below are wave-uniform).
+constexpr int kDQ = 256;   // ring capacity: pending <= 63 before up to two pushes of <= 64 (trial_pair)
+struct DirectQ {
+  // the pushes (ds_write) and the run's reads (ds_read) of other lanes' entries address the same
+  // array, so they stay in program order, and a wave's LDS operations execute in order: no
+  // memory fence (a fence would also order, and so de-scalarise, the caller's global loads)
+  float* buf;              // this wave's [3][kDQ] in LDS
+  int head, tail;          // wave-uniform counters
+  // pass 0 with the gate's hint set (its previous exponent was past the first window): the
+  // per-candidate elements also accumulate their Taylor polynomial, valid for k >= kTrialJ, into
+  // p16 ([kPolyHiN + 1][64] per wave in LDS, lane-indexed) so that k_select can decide
+  // exponents past the window without another pass
+  float* p16 = nullptr;
+  bool hi = false;
+};
+constexpr int kDQLds = 3 * kDQ + (kPolyHiN + 1) * 64;   // floats of one wave's queue + p16
+
+// enable the p16 polynomial for this block (pass 0, gate hint set: found[8 + q], k_reduce_g)
+__device__ __forceinline__ void dq_hint(DirectQ& dq, int pass, const int* found, int q) {
+  dq.p16 = dq.buf + 3 * kDQ;
+  dq.hi = pass == 0 && found[8 + q] != 0;
+  if (dq.hi) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int m = 0; m <= kPolyHiN; ++m) dq.p16[m * 64 + lane] = 0.f;
+  }
+}
 
 // sw = f2 sg w (the pushed entry): w = |z| (sigmoid) or 2|z| (tanh) with the sign of z; E and
 // r = sigma(w) are re-formed here exactly as trial_point / trial_pair formed them
 template <bool TANH>
-__device__ __forceinline__ void direct_candidates(float sw, float e, float d2, float (&acc)[kSlots]) {
+__device__ __forceinline__ void direct_candidates(float sw, float e, float d2, float (&acc)[kSlots], const DirectQ& dq) {
   const float w = fabsf(sw);
   const float E = __expf(-w);
   const float r = __builtin_amdgcn_rcpf(1.f + E);
-  const float cr = -(sw >= 0.f ? (TANH ? 2.f : 1.f) : (TANH ? -2.f : -1.f)) * r;
+  const float F = sw >= 0.f ? (TANH ? 2.f : 1.f) : (TANH ? -2.f : -1.f);   // D = F (sigma(w + eps) - sigma(w))
+  const float cr = -F * r;
+  if (dq.hi) {
+    // the element's Taylor polynomial in s for k >= kTrialJ: D = sum_n a_n s^n, a_n = F c_n(w) E0^n,
+    // E0 = e 2^(J-1) = F q (pass 0), valid while |E0| s <= 2^-5; remainder coefficients of s^2..s^10
+    const int lane = threadIdx.x & 63;
+    const float E0 = e * (float)(1 << (kTrialJ - 1));
+    if (fabsf(E0) <= kPolyQ * (float)(1 << kTrialJ)) {
+      const float sc = E * r;                       // 1 - sigma(w)
+      const float p = r * sc, h = sc - r;           // sigma', 1 - 2 sigma
+      const float e2 = E0 * E0;
+      const float a1 = F * p * E0, a2 = F * (0.5f * p * h) * e2, a3 = F * (p * (1.f - 6.f * p) * (1.f / 6.f)) * e2 * E0;
+      const float a4 = F * (p * h * (1.f - 12.f * p) * (1.f / 24.f)) * e2 * e2;
+      const float a5 = F * (p * (1.f - 30.f * p + 120.f * p * p) * (1.f / 120.f)) * e2 * e2 * E0;
+      const float t = d2;
+      float* P = dq.p16 + lane;
+      P[0 * 64] += fmaf(t, a2, a1 * a1);
+      P[1 * 64] += fmaf(t, a3, 2.f * a1 * a2);
+      P[2 * 64] += fmaf(t, a4, fmaf(2.f * a1, a3, a2 * a2));
+      P[3 * 64] += fmaf(t, a5, 2.f * fmaf(a1, a4, a2 * a3));
+      P[4 * 64] += fmaf(2.f * a1, a5, fmaf(2.f * a2, a4, a3 * a3));
+      P[5 * 64] += 2.f * fmaf(a2, a5, a3 * a4);
+      P[6 * 64] += fmaf(2.f * a3, a5, a4 * a4);
+      P[7 * 64] += 2.f * a4 * a5;
+      P[8 * 64] += a5 * a5;
+    } else {
+      dq.p16[kPolyHiN * 64 + lane] += 1.f;
+    }
+  }
   constexpr float kCap = 1e30f;
   float m = fminf(expm1_acc(-e), kCap);
   const float one_e = 1.f + E;
@@ -1167,21 +1233,6 @@ __device__ __forceinline__ void direct_candidates(float sw, float e, float d2, f
   }
 }
 
-// Per-wave queue of the elements in the per-candidate regime.  Which elements need the
-// 16-candidate loop is data dependent (on C3, 0-95 % per gate), so evaluating it in place
-// would run the loop for the whole wave whenever any lane needs it.  Instead each element's
-// five inputs are appended (ballot + prefix count) to an LDS ring of this wave, and the
-// loop runs once 64 entries are pending, with every lane busy.  All lanes of a wave must
-// make the same sequence of dq_push / dq_run calls (loops below are wave-uniform).
-constexpr int kDQ = 256;   // ring capacity: pending <= 63 before up to two pushes of <= 64 (trial_pair)
-struct DirectQ {
-  // the pushes (ds_write) and the run's reads (ds_read) of other lanes' entries address the same
-  // array, so they stay in program order, and a wave's LDS operations execute in order: no
-  // memory fence (a fence would also order, and so de-scalarise, the caller's global loads)
-  float* buf;              // this wave's [3][kDQ] in LDS
-  int head, tail;          // wave-uniform counters
-};
-
 // An entry is (sw, e, d2): sw = the signed w (E, r and the sign are re-formed from it when the
 // entry runs, one v_exp and one v_rcp per 64 entries instead of two more LDS words per push).
 __device__ __forceinline__ void dq_push(DirectQ& dq, bool p, float sw, float e, float d2) {
@@ -1208,9 +1259,15 @@ __device__ __forceinline__ void dq_run(DirectQ& dq, float (&acc)[kSlots], bool f
     const int n = dq.tail - dq.head < 64 ? dq.tail - dq.head : 64;
     if (lane < n) {
       const int slot = (dq.head + lane) & (kDQ - 1);
-      direct_candidates<TANH>(dq.buf[slot], dq.buf[kDQ + slot], dq.buf[2 * kDQ + slot], acc);
+      direct_candidates<TANH>(dq.buf[slot], dq.buf[kDQ + slot], dq.buf[2 * kDQ + slot], acc, dq);
     }
     dq.head += n;
+  }
+  if (final && dq.hi) {   // the lane's p16 sums into the block's slots
+    __builtin_amdgcn_wave_barrier();
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int m = 0; m <= kPolyHiN; ++m) acc[kSlotP16 + m] += dq.p16[m * 64 + lane];
   }
 }
 
@@ -1441,8 +1498,9 @@ __global__ __launch_bounds__(kThreads) void k_trial(Geom g, int pass, const floa
   float acc[kSlots];
 #pragma unroll
   for (int k = 0; k < kSlots; ++k) acc[k] = 0.f;
-  __shared__ float dqbuf[kThreads / 64][3 * kDQ];
+  __shared__ float dqbuf[kThreads / 64][kDQLds];
   DirectQ dq{dqbuf[threadIdx.x >> 6], 0, 0};
+  dq_hint(dq, pass, found, q);
   const bool vec = (g.H % 4) == 0;
   if (q == 2) {
     if (vec) trial_loop<true, 4>(n, zq, tq, Qq, pass, blk, nblk, acc, dq);
@@ -1617,8 +1675,9 @@ __global__ __launch_bounds__(kThreads, TF_MINB) void k_trial_fast(Geom g, int pa
   float acc[kSlots];
 #pragma unroll
   for (int k = 0; k < kSlots; ++k) acc[k] = 0.f;
-  __shared__ float dqbuf[kThreads / 64][3 * kDQ];
+  __shared__ float dqbuf[kThreads / 64][kDQLds];
   DirectQ dq{dqbuf[threadIdx.x >> 6], 0, 0};
+  dq_hint(dq, pass, found, q);
   if (q == 2) trial_fast_body<true, SIDE, DP, XV, UR>(g, q, pass, zc, tgt, Q, x, wlds, blk, nblk, acc, dq);
   else trial_fast_body<false, SIDE, DP, XV, UR>(g, q, pass, zc, tgt, Q, x, wlds, blk, nblk, acc, dq);
   trial_block_store(acc, part, q, blk, nblk);
@@ -1791,9 +1850,10 @@ __global__ __launch_bounds__(kThreads) void k_trial_rows(Geom g, int pass, const
   float acc[kSlots];
 #pragma unroll
   for (int k = 0; k < kSlots; ++k) acc[k] = 0.f;
-  __shared__ float dqbuf[kThreads / 64][3 * kDQ];
+  __shared__ float dqbuf[kThreads / 64][kDQLds];
   __shared__ float4 dwl[SPEC ? DP / 4 * 256 : 1];
   DirectQ dq{dqbuf[threadIdx.x >> 6], 0, 0};
+  dq_hint(dq, pass, found, q);
   if (q == 2) trial_rows_body<true, SIDE, DP, XV, SPEC, QP>(g, q, pass, zc, tgt, Q, x, Gx, blk, nblk, acc, dq, sp, dwl);
   else trial_rows_body<false, SIDE, DP, XV, SPEC, QP>(g, q, pass, zc, tgt, Q, x, Gx, blk, nblk, acc, dq, sp, dwl);
   // the column blocks of one (blk, q) add into the same part slot row: blk index widened by z
@@ -1932,8 +1992,9 @@ __global__ __launch_bounds__(kThreads, TMX_MINB) void k_trial_mx(Geom g, int pas
   float acc[kSlots];
 #pragma unroll
   for (int k = 0; k < kSlots; ++k) acc[k] = 0.f;
-  __shared__ float dqbuf[kThreads / 64][3 * kDQ];
+  __shared__ float dqbuf[kThreads / 64][kDQLds];
   DirectQ dq{dqbuf[threadIdx.x >> 6], 0, 0};
+  dq_hint(dq, pass, found, q);
   if (q == 2) trial_mx_body<true, SPEC>(g, q, pass, zc, tgt, x, Gx, blk, nblk, acc, dq, sp);
   else trial_mx_body<false, SPEC>(g, q, pass, zc, tgt, x, Gx, blk, nblk, acc, dq, sp);
   trial_block_store(acc, part, q, blockIdx.z * nblk + blk, nblk * gridDim.z);
@@ -2097,7 +2158,7 @@ __global__ __launch_bounds__(kThreads) void k_trial_debug(int64_t n, int mode, i
   const int pass = kbase / kTrialJ;
   const bool tanh_gate = mode & 1, pair = mode & 2;
   // the polynomial slots are only filled on pass 0: run pass 0 for them, then this pass
-  __shared__ float dqbuf[kThreads / 64][3 * kDQ];
+  __shared__ float dqbuf[kThreads / 64][kDQLds];
   DirectQ dq{dqbuf[threadIdx.x >> 6], 0, 0};
   auto run = [&](int ps, float (&a)[kSlots]) {
     if (pair) {
@@ -2270,6 +2331,24 @@ __global__ __launch_bounds__(kThreads) void k_select(Geom g, Hyper hp, SelectArg
       if (lhs > rhs) continue;
       pick = kk;
       break;
+    }
+    // pass 0, no exponent in the window, hint set and every per-candidate element covered by its
+    // polynomial past the window (dq_hint): decide k in [kTrialJ, kMaxK) from both polynomials
+    // (the s^1 slot only holds the per-candidate elements' linearisation, which the candidate sums
+    // needed: left out here, as the remainder has no s^1 term)
+    if (pick < 0 && a.pass == 0 && !poly_only && a.found_in[8 + q] && sm[kSlotN16] == 0.0) {
+      for (int kk = kTrialJ; kk < kMaxK; ++kk) {
+        const double sk = ldexp(1.0, -kk);
+        double poly = 0.0;
+        for (int n = kPolyN - 1; n >= 1; --n) poly = (poly + pl[n] + sm[kSlotP16 + n - 1]) * sk;
+        poly *= sk;
+        const double lhs = 0.5 * (double)rho * poly;
+        const double rhs = 0.5 * g.T * gsq * sk;
+        if (!isfinite(lhs) && mb == 0) atomicAdd(&a.stats->nonfinite, 1);
+        if (lhs > rhs) continue;
+        pick = kk;
+        break;
+      }
     }
     const int own = pick;   // -1: not decided within this pass's window
     if (a.force) {          // test hook: take the given exponent (the search above still ran)
@@ -2801,10 +2880,11 @@ void launch_atr(const Geom& g, int side, const float* x, const float* Sh, const 
 }
 
 void launch_reduce_g(const Geom& g, int side, const Hyper& hp, const float* slab, int nsplit, float* G, int* found,
-                     int* kpred, const DevStats* stats, hipStream_t s) {
+                     int* kpred, const DevStats* stats, hipStream_t s, bool p16) {
   const int Kd = side == 0 ? g.D : g.H;
   const int64_t n = 4LL * Kd * g.H;
-  k_reduce_g<<<cdiv64(n, kThreads), kThreads, 0, s>>>(Kd, g.H, hp, slab, nsplit, G, found, kpred, stats);
+  k_reduce_g<<<cdiv64(n, kThreads), kThreads, 0, s>>>(Kd, g.H, side, p16 ? 1 : 0, hp, slab, nsplit, G, found, kpred,
+                                                       stats);
 }
 
 void launch_qgemm(const Geom& g, int side, const float* x, const float* Sh, const float* G, float* Q,

@@ -10,7 +10,10 @@ constexpr int kTrialJ = 16;      // line-search candidates evaluated per trial p
 // per-gate sums of a trial pass: [J candidates][10 polynomial coefficients][sum d0^2][#per-candidate elements]
 constexpr int kPolyN = 10;
 constexpr float kPolyQ = 0x1p-5f;   // |q| bound of the polynomial (5-term Taylor) regime
-constexpr int kTrialSlots = kTrialJ + kPolyN + 2;
+// + pass 0's second polynomial (kPolyHiN coefficients of s^2..s^10 over the per-candidate
+// elements, valid for k >= kTrialJ) and the count of elements it cannot cover
+constexpr int kPolyHiN = 9;
+constexpr int kTrialSlots = kTrialJ + kPolyN + 2 + kPolyHiN + 1;
 constexpr int kMaxK = 96;        // exponents decided from the polynomial alone go up to this
 constexpr int kMaxPasses = 4;    // => exponents k in [0, 64)
 constexpr int kFastD = 16;       // fused weight-stage path for input_size <= 16
@@ -145,7 +148,8 @@ void launch_atr(const Geom& g, int side, const float* x, const float* Sh, const 
 // kpred (nullable, side 0): receives the previous step's x-side exponents from stats (SpecX)
 void launch_reduce_g(const Geom& g, int side, const Hyper& hp, const float* Gslab, int nsplit, float* G, int* found,
                      int* kpred, const DevStats* stats,
-                     hipStream_t s);
+                     hipStream_t s,
+                     bool p16 = true);
 // Q[q][row][j] = sum_m A[row][m] * G[q][m][j]
 void launch_qgemm(const Geom& g, int side, const float* x, const float* Sh, const float* G, float* Q,
                   hipStream_t s);

@@ -60,6 +60,8 @@ CASES = {
     # BASELINE configs at full size (compact: inputs as generator recipe + sha256, no state)
     'c3':           ('admm', False, 'uniform', 8192, 32, 16, 256, 5, False, 'GoogleStock'),
     'c5_1gpu':      ('no_dual_y', False, 'rw', 4096, 64, 1, 512, 3, False, 'GoogleStock'),
+    # C4's global problem (65536 samples; the 8-GPU run shards exactly this) on one device
+    'c4g':          ('admm', False, 'uniform', 65536, 32, 16, 256, 3, False, 'GoogleStock'),
 }
 
 # compact cases: which steps keep their full weights (the others keep x2q/out in full and
@@ -67,7 +69,8 @@ CASES = {
 # once by the fp64 oracle (oracle.admm_oracle.fp64_decisions) to record how the reference's
 # fp32 line-search decisions compare with fp64 ones from the same state
 COMPACT = {'c3': {'full_w': (1, 2, 3, 4, 5), 'fp64': True},
-           'c5_1gpu': {'full_w': (3,), 'fp64': False}}
+           'c5_1gpu': {'full_w': (3,), 'fp64': False},
+           'c4g': {'full_w': (3,), 'fp64': False}}
 WSTRIDE = 16
 
 

@@ -862,6 +862,41 @@ def test_q_two_piece_split_same_trajectory(shape, pieces, mods, dev, monkeypatch
     assert torch.equal(out[0][1], out[1][1])
 
 
+@pytest.mark.parametrize('shape,variant', [((32768, 4, 16, 256), 'admm'), ((40000, 3, 5, 64), 'admm')])
+def test_p16_decides_past_first_window(shape, variant, mods, dev, monkeypatch):
+    """Exponents k >= 16 (past pass 0's per-candidate window; the g gate at batch >= 16384, i.e.
+    C4's global 65536): with the gate's hint set (its last exponent was >= 16) pass 0 also sums
+    the per-candidate elements' polynomial valid past the window, and k_select decides there
+    without pass 1.  Against ADMM_P16=0 (pass 1 evaluates the window [16, 32) per candidate):
+    the same exponents at every step, bitwise equal trajectories, and some exponent >= 16."""
+    from blocks.lstm import LSTM
+    from parameters import example_parameter_dictionary
+    admm, _ = mods
+    admm.with_dual_y = False
+    B, T, D, H = shape
+    g = torch.Generator().manual_seed(37)
+    x = torch.rand(B, T, D, generator=g).to(dev)
+    y = (0.8 * x.mean((1, 2)).unsqueeze(1) + 0.1 * torch.rand(B, 1, generator=g).to(dev)).contiguous()
+    out = []
+    for mode in ('0', '1'):
+        monkeypatch.setenv('ADMM_P16', mode)
+        torch.manual_seed(0)
+        m = LSTM(D, H, 1).to(dev)
+        opt = admm.ADMMBasedOptimizer(m, (x, y), example_parameter_dictionary['GoogleStock'], verbose=False)
+        ks, passes = [], []
+        for _ in range(4):
+            opt.step()
+            st = opt.last_step_stats()
+            ks.append(list(st['k'].values()))
+            passes.append(st['passes'])
+        out.append((ks, passes, torch.cat([p.detach().flatten() for p in m.parameters()]
+                                          + [v.flatten() for v in opt.gates.values()])))
+        del opt
+    assert out[0][0] == out[1][0], (out[0][0], out[1][0])
+    assert max(max(k) for k in out[1][0][1:]) >= 16, out[1][0]
+    assert torch.equal(out[0][2], out[1][2])
+
+
 @pytest.mark.parametrize('shape', [(1000, 5, 16, 256), (300, 4, 1, 512)])
 def test_q_bf16_storage_same_trajectory(shape, mods, dev, monkeypatch):
     """Q stored in bf16 (ADMM_QPAIR=2, the default) against f32 (ADMM_QPAIR=1), the same row-quad

@@ -140,6 +140,7 @@ struct AdmmCtx {
   hipStream_t sx[kMaxSweepStreams - 1] = {};
   hipEvent_t ev_fork = nullptr, ev_join[kMaxSweepStreams - 1] = {};
   float *U = nullptr, *wy_slab = nullptr, *Gy = nullptr;
+  bool gy_pending = false;   // G_y waits in gy_slot for the x stage's all-reduce (several processes)
   int wy_nsplit = 1;
   double *ht_part = nullptr, *ht_sums = nullptr;
   int ht_nblk = 1;
@@ -246,6 +247,9 @@ int allreduce_f64(AdmmCtx* c, double* p, size_t n, hipStream_t s) {
   return ADMM_OK;
 }
 
+// G_y's slot after the x stage's G [4][D][H] (the G buffer holds 4 max(D, H) H + H O floats)
+float* gy_slot(AdmmCtx* c) { return c->G + (size_t)4 * c->g.D * c->g.H; }
+
 // wy update (admm.py:246-280; admm.no_dual_y.py:226-249)
 int stage_wy(AdmmCtx* c, hipStream_t s) {
   const Geom& g = c->g;
@@ -256,10 +260,10 @@ int stage_wy(AdmmCtx* c, hipStream_t s) {
     launch_wy_reduce(g, c->hp, c->wy_slab, c->wy_nsplit, c->Gy, c->buf.wy, s);
     return ADMM_OK;
   }
-  launch_wy_reduce(g, c->hp, c->wy_slab, c->wy_nsplit, c->Gy, nullptr, s);
-  int rc = allreduce_f32(c, c->Gy, (size_t)g.H * g.O, s);
-  if (rc) return rc;
-  launch_wy_apply(g, c->hp, c->Gy, c->buf.wy, s);
+  // several processes: G_y is all-reduced together with the x stage's G (the x stage does not
+  // read wy), in the slot right after it, and wy is updated once that all-reduce is done
+  launch_wy_reduce(g, c->hp, c->wy_slab, c->wy_nsplit, gy_slot(c), nullptr, s);
+  c->gy_pending = true;
   return ADMM_OK;
 }
 
@@ -318,8 +322,15 @@ int stage_weights(AdmmCtx* c, int side, hipStream_t s) {
   }
   launch_reduce_g(g, side, c->hp, gsrc, ns, c->G, c->found, spec && side == 0 ? c->kpred : nullptr, c->stats, s,
                   c->p16);
-  int rc = allreduce_f32(c, c->G, (size_t)4 * Kd * g.H, s);
+  // (x stage with G_y pending: one all-reduce for both, then the wy update)
+  const bool with_gy = side == 0 && c->gy_pending;
+  int rc = allreduce_f32(c, c->G, (size_t)4 * Kd * g.H + (with_gy ? (size_t)g.H * g.O : 0), s);
   if (rc) return rc;
+  if (with_gy) {
+    ProfScope ps(c, ADMM_PROF_SMALL, s);
+    launch_wy_apply(g, c->hp, gy_slot(c), c->buf.wy, s);
+    c->gy_pending = false;
+  }
   if (c->trace_g[side])
     HIP_TRY(hipMemcpyAsync(c->trace_g[side], c->G, (size_t)4 * Kd * g.H * sizeof(float), hipMemcpyDeviceToDevice, s));
   // 2. trial direction Q = A G (not needed on the fast x side: formed inside the trials)
@@ -345,9 +356,13 @@ int stage_weights(AdmmCtx* c, int side, hipStream_t s) {
   // the row-pair trial kernel (H % 256 == 0) writes one partial per (block, column block)
   const int nred = fast && side == 0 && trial_mx_ok(g) ? nblk * (g.H / 128)
                    : fast && trial_rows_ok(g) ? nblk * (g.H / 256) : nblk;
-  for (int pass = 0; pass < kMaxPasses; ++pass) {
+  // pass 0, then the tail (windows 1 .. kMaxPasses - 1 in one launch, one selection, one
+  // all-reduce) for the gates pass 0 left undecided -- with the polynomial past the window
+  // (hint, k_reduce_g) that is rare, and the tail's workgroups exit at once
+  for (int pass : {0, kTailPass}) {
+    const int par = pass == 0 ? 0 : 1;   // parity of the found flags this pass reads
     {
-      ProfScope ps(c, pass > 0 ? ADMM_PROF_TRIAL_EXTRA : side == 0 ? ADMM_PROF_TRIAL : ADMM_PROF_TRIAL_H, s);
+      ProfScope ps(c, pass != 0 ? ADMM_PROF_TRIAL_EXTRA : side == 0 ? ADMM_PROF_TRIAL : ADMM_PROF_TRIAL_H, s);
       SpecX sx{};
       if (spec && side == 0 && pass == 0) {
         sx.kpred = c->kpred;
@@ -357,20 +372,21 @@ int stage_weights(AdmmCtx* c, int side, hipStream_t s) {
       }
       if (fast)
         launch_trial_fast(g, side, pass, side == 1 ? zh : c->zc, c->tgt, side == 1 ? c->Q : nullptr, c->buf.x,
-                          side == 0 ? c->G : c->dW, c->found + 4 * (pass & 1), c->tr_part, nblk, s, sx.zx ? &sx : nullptr,
+                          side == 0 ? c->G : c->dW, c->found + 4 * par, c->tr_part, nblk, s, sx.zx ? &sx : nullptr,
                           side == 1 && c->split3 ? c->qpair : 0);
       else
-        launch_trial(g, pass, c->zc, c->tgt, c->Q, c->found + 4 * (pass & 1), c->tr_part, nblk, s);
+        launch_trial(g, pass, c->zc, c->tgt, c->Q, c->found + 4 * par, c->tr_part, nblk, s);
     }
     sa.pass = pass;
-    sa.found_in = c->found + 4 * (pass & 1);
-    sa.found_out = c->found + 4 * ((pass + 1) & 1);
+    sa.found_in = c->found + 4 * par;
+    sa.found_out = c->found + 4 * (par ^ 1);
+    const int nwin = pass == 0 ? 1 : kMaxPasses - 1;
     if (fused_reduce) {   // k_select reduces the partials itself (no all-reduce in between)
       sa.part = c->tr_part;
       sa.nred = nred;
     } else {
       launch_trial_reduce(g, pass, c->tr_part, nred, sa.found_in, c->tr_sums, s);
-      rc = allreduce_f64(c, c->tr_sums, 4 * kTrialSlots, s);
+      rc = allreduce_f64(c, c->tr_sums, (size_t)nwin * 4 * kTrialSlots, s);
       if (rc) return rc;
       sa.part = nullptr;
     }
@@ -541,11 +557,11 @@ int admm_create(const AdmmDims* dims, const AdmmParams* params, int device, Admm
   c->wy_nsplit = wy_splits(g);
   c->ht_nblk = ht_blocks(g);
   if ((rc = dalloc(&c->zc, 4 * plane)) || (rc = dalloc(&c->tgt, 4 * plane)) || (rc = dalloc(&c->R, fast_path(g) && !c->force_generic ? 1 : 4 * plane)) ||
-      (rc = dalloc(&c->Q, 4 * plane)) || (rc = dalloc(&c->G, (size_t)4 * Kmax * g.H)) ||
+      (rc = dalloc(&c->Q, 4 * plane)) || (rc = dalloc(&c->G, (size_t)4 * Kmax * g.H + (size_t)g.H * g.O)) ||
       (rc = dalloc(&c->dW, (size_t)4 * g.D * g.H)) ||
       (rc = dalloc(&c->gslab, slab)) ||
-      (rc = dalloc(&c->tr_part, (size_t)4 * kTrialSlots * c->nblk_trial)) ||
-      (rc = dalloc(&c->tr_sums, (size_t)4 * kTrialSlots)) || (rc = dalloc(&c->tr_poly, (size_t)4 * kPolyN)) ||
+      (rc = dalloc(&c->tr_part, (size_t)(kMaxPasses - 1) * 4 * kTrialSlots * c->nblk_trial)) ||
+      (rc = dalloc(&c->tr_sums, (size_t)(kMaxPasses - 1) * 4 * kTrialSlots)) || (rc = dalloc(&c->tr_poly, (size_t)4 * kPolyN)) ||
       (rc = dalloc(&c->found, 12)) || (rc = dalloc(&c->pick, 4)) ||
       (rc = dalloc(&c->U, (size_t)g.B * g.O)) || (rc = dalloc(&c->wy_slab, (size_t)c->wy_nsplit * g.H * g.O)) ||
       (rc = dalloc(&c->Gy, (size_t)g.H * g.O)) || (rc = dalloc(&c->ht_part, (size_t)c->ht_nblk * kHTSums)) ||

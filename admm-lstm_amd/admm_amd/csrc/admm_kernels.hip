@@ -11,6 +11,7 @@
 
 #include "admm_dev.hpp"
 #include "admm_kernels.hpp"
+#include <type_traits>
 
 namespace admm {
 
@@ -1440,6 +1441,13 @@ __device__ __forceinline__ void trial_pair_fold(float (&acc)[kSlots], const f32x
   for (int n = 0; n < kPolyN; ++n) acc[kSlotPoly + n] += acc2[n + 1].x + acc2[n + 1].y;
 }
 
+// Trial kernels take pass >= 0 (one window) or pass = kTailPass: the tail, windows 1 ..
+// kMaxPasses - 1 one after the other in the same launch (their partials at part + (p - 1) times
+// 4 kSlots nred), for the gates pass 0 left undecided.  One launch, one selection and (multi-
+// process) one all-reduce replace three passes that almost never have work to do.
+__device__ __forceinline__ int pass_lo(int pass) { return pass == kTailPass ? 1 : pass; }
+__device__ __forceinline__ int pass_hi(int pass) { return pass == kTailPass ? kMaxPasses : pass + 1; }
+
 __device__ __forceinline__ void trial_block_store(float (&acc)[kSlots], double* part, int q, int blk, int nblk) {
   __shared__ double red[4][kSlots];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -1487,6 +1495,7 @@ __device__ __forceinline__ void trial_loop(int64_t n, const float* zq, const flo
   dq_run<TANH>(dq, acc, true);
 }
 
+template <bool TAIL>
 __global__ __launch_bounds__(kThreads) void k_trial(Geom g, int pass, const float* zc, const float* tgt,
                                                       const float* Q, const int* found, double* part, int nblk) {
   const int q = blockIdx.y, blk = blockIdx.x;  // gate-major: one code path per CU at a time (I-cache)
@@ -1495,21 +1504,24 @@ __global__ __launch_bounds__(kThreads) void k_trial(Geom g, int pass, const floa
   const float* zq = zc + (int64_t)q * n;
   const float* tq = tgt + (int64_t)q * n;
   const float* Qq = Q + (int64_t)q * n;
-  float acc[kSlots];
-#pragma unroll
-  for (int k = 0; k < kSlots; ++k) acc[k] = 0.f;
   __shared__ float dqbuf[kThreads / 64][kDQLds];
-  DirectQ dq{dqbuf[threadIdx.x >> 6], 0, 0};
-  dq_hint(dq, pass, found, q);
   const bool vec = (g.H % 4) == 0;
-  if (q == 2) {
-    if (vec) trial_loop<true, 4>(n, zq, tq, Qq, pass, blk, nblk, acc, dq);
-    else trial_loop<true, 1>(n, zq, tq, Qq, pass, blk, nblk, acc, dq);
-  } else {
-    if (vec) trial_loop<false, 4>(n, zq, tq, Qq, pass, blk, nblk, acc, dq);
-    else trial_loop<false, 1>(n, zq, tq, Qq, pass, blk, nblk, acc, dq);
+  for (int ps = TAIL ? 1 : pass; ps < (TAIL ? kMaxPasses : pass + 1); ++ps) {
+    float acc[kSlots];
+#pragma unroll
+    for (int k = 0; k < kSlots; ++k) acc[k] = 0.f;
+    DirectQ dq{dqbuf[threadIdx.x >> 6], 0, 0};
+    dq_hint(dq, ps, found, q);
+    if (q == 2) {
+      if (vec) trial_loop<true, 4>(n, zq, tq, Qq, ps, blk, nblk, acc, dq);
+      else trial_loop<true, 1>(n, zq, tq, Qq, ps, blk, nblk, acc, dq);
+    } else {
+      if (vec) trial_loop<false, 4>(n, zq, tq, Qq, ps, blk, nblk, acc, dq);
+      else trial_loop<false, 1>(n, zq, tq, Qq, ps, blk, nblk, acc, dq);
+    }
+    trial_block_store(acc, part + (int64_t)(ps - (TAIL ? 1 : pass)) * 4 * kSlots * nblk, q, blk, nblk);
+    __syncthreads();
   }
-  trial_block_store(acc, part, q, blk, nblk);
 }
 
 // Fast trial pass (D <= kFastD, H % 4 == 0): rows x float4 columns.  Side 0 forms the trial
@@ -1664,7 +1676,7 @@ __device__ __forceinline__ void trial_fast_body(const Geom& g, int q, int pass, 
 #ifndef TF_MINB
 #define TF_MINB 1   // workgroups per CU the register allocation must allow (occupancy for the streams)
 #endif
-template <int SIDE, int DP, bool XV, bool UR>
+template <int SIDE, int DP, bool XV, bool UR, bool TAIL = false>
 __global__ __launch_bounds__(kThreads, TF_MINB) void k_trial_fast(Geom g, int pass, const float* zc, const float* tgt,
                                                            const float* Q, const float* x, const float* Wsrc,
                                                            const int* found, double* part, int nblk) {
@@ -1672,15 +1684,25 @@ __global__ __launch_bounds__(kThreads, TF_MINB) void k_trial_fast(Geom g, int pa
   const int q = blockIdx.y, blk = blockIdx.x;  // gate-major: one code path per CU at a time (I-cache)
   if (found[q]) return;
   if (SIDE == 0) stage_wlds<DP>(g, Wsrc + (int64_t)q * g.D * g.H, wlds);
-  float acc[kSlots];
-#pragma unroll
-  for (int k = 0; k < kSlots; ++k) acc[k] = 0.f;
   __shared__ float dqbuf[kThreads / 64][kDQLds];
-  DirectQ dq{dqbuf[threadIdx.x >> 6], 0, 0};
-  dq_hint(dq, pass, found, q);
-  if (q == 2) trial_fast_body<true, SIDE, DP, XV, UR>(g, q, pass, zc, tgt, Q, x, wlds, blk, nblk, acc, dq);
-  else trial_fast_body<false, SIDE, DP, XV, UR>(g, q, pass, zc, tgt, Q, x, wlds, blk, nblk, acc, dq);
-  trial_block_store(acc, part, q, blk, nblk);
+  auto one = [&](int ps, double* pp) {
+    float acc[kSlots];
+#pragma unroll
+    for (int k = 0; k < kSlots; ++k) acc[k] = 0.f;
+    DirectQ dq{dqbuf[threadIdx.x >> 6], 0, 0};
+    dq_hint(dq, ps, found, q);
+    if (q == 2) trial_fast_body<true, SIDE, DP, XV, UR>(g, q, ps, zc, tgt, Q, x, wlds, blk, nblk, acc, dq);
+    else trial_fast_body<false, SIDE, DP, XV, UR>(g, q, ps, zc, tgt, Q, x, wlds, blk, nblk, acc, dq);
+    trial_block_store(acc, pp, q, blk, nblk);
+  };
+  if constexpr (TAIL) {
+    for (int ps = 1; ps < kMaxPasses; ++ps) {
+      one(ps, part + (int64_t)(ps - 1) * 4 * kSlots * nblk);
+      __syncthreads();
+    }
+  } else {
+    one(pass, part);
+  }
 }
 
 // Trial pass for H % 256 == 0 (the C3/C4/C5 shapes): a workgroup owns 256 columns j, one per
@@ -1839,7 +1861,7 @@ __device__ __forceinline__ void trial_rows_body(const Geom& g, int q, int pass, 
   dq_run<TANH>(dq, acc, true);
 }
 
-template <int SIDE, int DP, bool XV, bool SPEC, int QP = 0>
+template <int SIDE, int DP, bool XV, bool SPEC, int QP = 0, bool TAIL = false>
 __global__ __launch_bounds__(kThreads) void k_trial_rows(Geom g, int pass, const float* __restrict__ zc,
                                                          const float* __restrict__ tgt, const float* __restrict__ Q,
                                                          const float* __restrict__ x, const float* __restrict__ Gx,
@@ -1847,17 +1869,28 @@ __global__ __launch_bounds__(kThreads) void k_trial_rows(Geom g, int pass, const
                                                          int nblk, SpecX sp) {
   const int q = blockIdx.y, blk = blockIdx.x;
   if (found[q]) return;
-  float acc[kSlots];
-#pragma unroll
-  for (int k = 0; k < kSlots; ++k) acc[k] = 0.f;
   __shared__ float dqbuf[kThreads / 64][kDQLds];
   __shared__ float4 dwl[SPEC ? DP / 4 * 256 : 1];
-  DirectQ dq{dqbuf[threadIdx.x >> 6], 0, 0};
-  dq_hint(dq, pass, found, q);
-  if (q == 2) trial_rows_body<true, SIDE, DP, XV, SPEC, QP>(g, q, pass, zc, tgt, Q, x, Gx, blk, nblk, acc, dq, sp, dwl);
-  else trial_rows_body<false, SIDE, DP, XV, SPEC, QP>(g, q, pass, zc, tgt, Q, x, Gx, blk, nblk, acc, dq, sp, dwl);
   // the column blocks of one (blk, q) add into the same part slot row: blk index widened by z
-  trial_block_store(acc, part, q, blockIdx.z * nblk + blk, nblk * gridDim.z);
+  const int nred = nblk * gridDim.z;
+  auto one = [&](int ps, double* pp) {
+    float acc[kSlots];
+#pragma unroll
+    for (int k = 0; k < kSlots; ++k) acc[k] = 0.f;
+    DirectQ dq{dqbuf[threadIdx.x >> 6], 0, 0};
+    dq_hint(dq, ps, found, q);
+    if (q == 2) trial_rows_body<true, SIDE, DP, XV, SPEC, QP>(g, q, ps, zc, tgt, Q, x, Gx, blk, nblk, acc, dq, sp, dwl);
+    else trial_rows_body<false, SIDE, DP, XV, SPEC, QP>(g, q, ps, zc, tgt, Q, x, Gx, blk, nblk, acc, dq, sp, dwl);
+    trial_block_store(acc, pp, q, blockIdx.z * nblk + blk, nred);
+  };
+  if constexpr (TAIL) {
+    for (int ps = 1; ps < kMaxPasses; ++ps) {
+      one(ps, part + (int64_t)(ps - 1) * 4 * kSlots * nred);
+      __syncthreads();
+    }
+  } else {
+    one(pass, part);
+  }
 }
 
 // x-side trial pass on the matrix cores (H % 128 == 0, D <= 16): each wave owns a 32-column
@@ -1982,22 +2015,33 @@ __device__ __forceinline__ void trial_mx_body(const Geom& g, int q, int pass, co
 #ifndef TMX_MINB
 #define TMX_MINB 4   // 4 waves/SIMD (128 VGPRs), the next tile prefetched in place (TMX_ROLL)
 #endif
-template <bool SPEC>
+template <bool SPEC, bool TAIL = false>
 __global__ __launch_bounds__(kThreads, TMX_MINB) void k_trial_mx(Geom g, int pass, const float* __restrict__ zc,
                                                        const float* __restrict__ tgt, const float* __restrict__ x,
                                                        const float* __restrict__ Gx, const int* __restrict__ found,
                                                        double* __restrict__ part, int nblk, SpecX sp) {
   const int q = blockIdx.y, blk = blockIdx.x;
   if (found[q]) return;
-  float acc[kSlots];
-#pragma unroll
-  for (int k = 0; k < kSlots; ++k) acc[k] = 0.f;
   __shared__ float dqbuf[kThreads / 64][kDQLds];
-  DirectQ dq{dqbuf[threadIdx.x >> 6], 0, 0};
-  dq_hint(dq, pass, found, q);
-  if (q == 2) trial_mx_body<true, SPEC>(g, q, pass, zc, tgt, x, Gx, blk, nblk, acc, dq, sp);
-  else trial_mx_body<false, SPEC>(g, q, pass, zc, tgt, x, Gx, blk, nblk, acc, dq, sp);
-  trial_block_store(acc, part, q, blockIdx.z * nblk + blk, nblk * gridDim.z);
+  const int nred = nblk * gridDim.z;
+  auto one = [&](int ps, double* pp) {
+    float acc[kSlots];
+#pragma unroll
+    for (int k = 0; k < kSlots; ++k) acc[k] = 0.f;
+    DirectQ dq{dqbuf[threadIdx.x >> 6], 0, 0};
+    dq_hint(dq, ps, found, q);
+    if (q == 2) trial_mx_body<true, SPEC>(g, q, ps, zc, tgt, x, Gx, blk, nblk, acc, dq, sp);
+    else trial_mx_body<false, SPEC>(g, q, ps, zc, tgt, x, Gx, blk, nblk, acc, dq, sp);
+    trial_block_store(acc, pp, q, blockIdx.z * nblk + blk, nred);
+  };
+  if constexpr (TAIL) {
+    for (int ps = 1; ps < kMaxPasses; ++ps) {
+      one(ps, part + (int64_t)(ps - 1) * 4 * kSlots * nred);
+      __syncthreads();
+    }
+  } else {
+    one(pass, part);
+  }
 }
 
 // After the x stage: zc += X dWx, so the h stage sees z = X Wx_new + Hprev Wh
@@ -2199,8 +2243,10 @@ __global__ __launch_bounds__(kThreads) void k_trial_debug(int64_t n, int mode, i
 __global__ __launch_bounds__(kThreads) void k_trial_reduce(int pass, const double* part, int nblk, const int* found,
                                                              double* sums) {
   __shared__ double red[4];
-  const int k = blockIdx.x, q = blockIdx.y;      // one block per (slot, gate)
+  const int k = blockIdx.x, q = blockIdx.y;      // one block per (slot, gate[, tail window z])
   if (found[q]) return;
+  part += (int64_t)blockIdx.z * 4 * kSlots * nblk;
+  sums += (int64_t)blockIdx.z * 4 * kSlots;
   double s = 0.0;
   const double* p = part + ((int64_t)q * kSlots + k) * nblk;
   for (int i = threadIdx.x; i < nblk; i += kThreads) s += p[i];
@@ -2242,37 +2288,6 @@ __global__ __launch_bounds__(kThreads) void k_select(Geom g, Hyper hp, SelectArg
     }
     return;
   }
-  // 1. the pass sums of this gate
-  if (a.part) {
-    double acc[kSlots];
-#pragma unroll
-    for (int k = 0; k < kSlots; ++k) acc[k] = 0.0;
-    const double* p = a.part + (int64_t)q * kSlots * a.nred;
-    int i = tid;
-    for (; i + kThreads < a.nred; i += 2 * kThreads) {   // two partials' loads in flight, same sum order
-      double v0[kSlots], v1[kSlots];
-#pragma unroll
-      for (int k = 0; k < kSlots; ++k) {
-        v0[k] = p[(int64_t)k * a.nred + i];
-        v1[k] = p[(int64_t)k * a.nred + i + kThreads];
-      }
-#pragma unroll
-      for (int k = 0; k < kSlots; ++k) acc[k] = (acc[k] + v0[k]) + v1[k];
-    }
-    if (i < a.nred) {
-#pragma unroll
-      for (int k = 0; k < kSlots; ++k) acc[k] += p[(int64_t)k * a.nred + i];
-    }
-#pragma unroll
-    for (int k = 0; k < kSlots; ++k) {
-      const double v = wave_sum(acc[k]);
-      if (lane == 0) red[w][k] = v;
-    }
-    __syncthreads();
-    if (tid < kSlots) sums[tid] = (red[0][tid] + red[1][tid]) + (red[2][tid] + red[3][tid]);
-  } else if (tid < kSlots) {
-    sums[tid] = a.sums[q * kSlots + tid];
-  }
   // 2. ||G||^2 (k_decide's order: float4 loads 8 at a time)
   const int Kd = a.side == 0 ? g.D : g.H;
   const int64_t nW = (int64_t)Kd * g.H;
@@ -2306,18 +2321,53 @@ __global__ __launch_bounds__(kThreads) void k_select(Geom g, Hyper hp, SelectArg
   } else {
     for (int64_t i = tid; i < nW; i += kThreads) gs += (double)Gq[i] * (double)Gq[i];
   }
-  const double gsq = block_sum(gs, gred);   // (its barriers also publish sums[])
+  const double gsq = block_sum(gs, gred);
   const float rho = hp.rho[q];
+  // per window (one, or the tail's windows 1 .. kMaxPasses - 1 in order until one decides)
+  for (int ps = pass_lo(a.pass); ps < pass_hi(a.pass); ++ps) {
+  const int64_t wofs = (int64_t)(ps - pass_lo(a.pass)) * 4 * kSlots;
+  // 1. the window's sums of this gate
+  if (a.part) {
+    double acc[kSlots];
+#pragma unroll
+    for (int k = 0; k < kSlots; ++k) acc[k] = 0.0;
+    const double* p = a.part + wofs * a.nred + (int64_t)q * kSlots * a.nred;
+    int i = tid;
+    for (; i + kThreads < a.nred; i += 2 * kThreads) {   // two partials' loads in flight, same sum order
+      double v0[kSlots], v1[kSlots];
+#pragma unroll
+      for (int k = 0; k < kSlots; ++k) {
+        v0[k] = p[(int64_t)k * a.nred + i];
+        v1[k] = p[(int64_t)k * a.nred + i + kThreads];
+      }
+#pragma unroll
+      for (int k = 0; k < kSlots; ++k) acc[k] = (acc[k] + v0[k]) + v1[k];
+    }
+    if (i < a.nred) {
+#pragma unroll
+      for (int k = 0; k < kSlots; ++k) acc[k] += p[(int64_t)k * a.nred + i];
+    }
+#pragma unroll
+    for (int k = 0; k < kSlots; ++k) {
+      const double v = wave_sum(acc[k]);
+      if (lane == 0) red[w][k] = v;
+    }
+    __syncthreads();
+    if (tid < kSlots) sums[tid] = (red[0][tid] + red[1][tid]) + (red[2][tid] + red[3][tid]);
+  } else if (tid < kSlots) {
+    sums[tid] = a.sums[wofs + q * kSlots + tid];
+  }
+  __syncthreads();
   // 3. the decision
   if (tid == 0) {
     const double* sm = sums;
     double* pq = a.poly + q * kPolyN;
     double pl[kPolyN];
-    for (int n = 0; n < kPolyN; ++n) pl[n] = a.pass == 0 ? sm[kSlotPoly + n] : pq[n];
-    if (a.pass == 0 && mb == 0)
+    for (int n = 0; n < kPolyN; ++n) pl[n] = ps == 0 ? sm[kSlotPoly + n] : pq[n];
+    if (ps == 0 && mb == 0)
       for (int n = 0; n < kPolyN; ++n) pq[n] = pl[n];
     const bool poly_only = sm[kSlotNne] == 0.0;
-    const int k_lo = poly_only ? 0 : a.pass * kTrialJ;
+    const int k_lo = poly_only ? 0 : ps * kTrialJ;
     const int k_hi = poly_only ? kMaxK : k_lo + kTrialJ;
     int pick = -1;
     for (int kk = k_lo; kk < k_hi; ++kk) {
@@ -2336,7 +2386,7 @@ __global__ __launch_bounds__(kThreads) void k_select(Geom g, Hyper hp, SelectArg
     // polynomial past the window (dq_hint): decide k in [kTrialJ, kMaxK) from both polynomials
     // (the s^1 slot only holds the per-candidate elements' linearisation, which the candidate sums
     // needed: left out here, as the remainder has no s^1 term)
-    if (pick < 0 && a.pass == 0 && !poly_only && a.found_in[8 + q] && sm[kSlotN16] == 0.0) {
+    if (pick < 0 && ps == 0 && !poly_only && a.found_in[8 + q] && sm[kSlotN16] == 0.0) {
       for (int kk = kTrialJ; kk < kMaxK; ++kk) {
         const double sk = ldexp(1.0, -kk);
         double poly = 0.0;
@@ -2353,7 +2403,7 @@ __global__ __launch_bounds__(kThreads) void k_select(Geom g, Hyper hp, SelectArg
     const int own = pick;   // -1: not decided within this pass's window
     if (a.force) {          // test hook: take the given exponent (the search above still ran)
       pick = a.force[2 * q + a.side];
-    } else if (pick < 0 && (poly_only || a.pass == a.last_pass)) {
+    } else if (pick < 0 && (poly_only || ps == kMaxPasses - 1)) {
       pick = k_hi;
       if (mb == 0) atomicAdd(&a.stats->unresolved, 1);
     }
@@ -2365,12 +2415,15 @@ __global__ __launch_bounds__(kThreads) void k_select(Geom g, Hyper hp, SelectArg
         a.stats->f_w[slot] = 0.5 * (double)rho * sm[kSlotFw];
         a.stats->grad_sq[slot] = gsq;
         a.stats->direct_frac[slot] = sm[kSlotNne] / ((double)g.Bg * g.T * g.H);
-        a.stats->passes[a.side] = a.pass + 1;
+        a.stats->passes[a.side] = ps + 1;
       }
       a.found_out[q] = pick >= 0 ? 1 : 0;
       a.pick[q] = pick;
     }
     pick_s = pick;
+  }
+  __syncthreads();
+  if (pick_s >= 0) break;
   }
   __syncthreads();
   const int pick = pick_s;
@@ -2907,7 +2960,8 @@ int trial_blocks(const Geom& g) {
 void launch_trial(const Geom& g, int pass, const float* zc, const float* tgt, const float* Q, const int* found,
                   double* part, int nblk, hipStream_t s) {
   dim3 grid(nblk, 4);
-  k_trial<<<grid, kThreads, 0, s>>>(g, pass, zc, tgt, Q, found, part, nblk);
+  if (pass == kTailPass) k_trial<true><<<grid, kThreads, 0, s>>>(g, pass, zc, tgt, Q, found, part, nblk);
+  else k_trial<false><<<grid, kThreads, 0, s>>>(g, pass, zc, tgt, Q, found, part, nblk);
 }
 
 void launch_trial_debug(int64_t n, int tanh_gate, int kbase, const float* z, const float* tgt, const float* q,
@@ -2918,7 +2972,7 @@ void launch_trial_debug(int64_t n, int tanh_gate, int kbase, const float* z, con
 void launch_trial_reduce(const Geom& g, int pass, const double* part, int nblk, const int* found, double* sums,
                          hipStream_t s) {
   (void)g;
-  k_trial_reduce<<<dim3(kSlots, 4), kThreads, 0, s>>>(pass, part, nblk, found, sums);
+  k_trial_reduce<<<dim3(kSlots, 4, pass == kTailPass ? kMaxPasses - 1 : 1), kThreads, 0, s>>>(pass, part, nblk, found, sums);
 }
 
 bool fast_path(const Geom& g) {
@@ -2989,47 +3043,53 @@ void launch_trial_fast(const Geom& g, int side, int pass, const float* zc, const
                        const SpecX* spec, int qpair) {
   dim3 grid(nblk, 4);
   const SpecX sp = spec ? *spec : SpecX{};
-  if (side == 1 && trial_rows_ok(g)) {
-    dim3 gr(nblk, 4, g.H / 256);
-    if (qpair == 2 && qpair_ok(g))
-      k_trial_rows<1, 4, false, false, 2><<<gr, kThreads, 0, s>>>(g, pass, zc, tgt, Q, x, Wsrc, found, part, nblk, sp);
-    else if (qpair == 1 && qpair_ok(g))
-      k_trial_rows<1, 4, false, false, 1><<<gr, kThreads, 0, s>>>(g, pass, zc, tgt, Q, x, Wsrc, found, part, nblk, sp);
-    else
-      k_trial_rows<1, 4, false, false><<<gr, kThreads, 0, s>>>(g, pass, zc, tgt, Q, x, Wsrc, found, part, nblk, sp);
-    return;
-  }
-  if (side == 1) {  // no x . W product on this side: one instantiation
-    k_trial_fast<1, 4, false, false><<<grid, kThreads, 0, s>>>(g, pass, zc, tgt, Q, x, Wsrc, found, part, nblk);
-    return;
-  }
-  if (trial_mx_ok(g)) {   // side 0 on the matrix cores
-    dim3 gr(nblk, 4, g.H / 128);
-    if (spec) k_trial_mx<true><<<gr, kThreads, 0, s>>>(g, pass, zc, tgt, x, Wsrc, found, part, nblk, sp);
-    else k_trial_mx<false><<<gr, kThreads, 0, s>>>(g, pass, zc, tgt, x, Wsrc, found, part, nblk, sp);
-    return;
-  }
-  if (trial_rows_ok(g)) {
-    dim3 gr(nblk, 4, g.H / 256);
-    with_dp(g, [&](auto dp, auto xv) {
-      if (spec)
-        k_trial_rows<0, decltype(dp)::value, decltype(xv)::value, true>
-            <<<gr, kThreads, 0, s>>>(g, pass, zc, tgt, Q, x, Wsrc, found, part, nblk, sp);
+  // TAIL: the windows 1 .. kMaxPasses - 1 in one launch (pass == kTailPass); only pass 0 speculates
+  auto go = [&](auto tail) {
+    constexpr bool TL = decltype(tail)::value;
+    if (side == 1 && trial_rows_ok(g)) {
+      dim3 gr(nblk, 4, g.H / 256);
+      if (qpair == 2 && qpair_ok(g))
+        k_trial_rows<1, 4, false, false, 2, TL><<<gr, kThreads, 0, s>>>(g, pass, zc, tgt, Q, x, Wsrc, found, part, nblk, sp);
+      else if (qpair == 1 && qpair_ok(g))
+        k_trial_rows<1, 4, false, false, 1, TL><<<gr, kThreads, 0, s>>>(g, pass, zc, tgt, Q, x, Wsrc, found, part, nblk, sp);
       else
-        k_trial_rows<0, decltype(dp)::value, decltype(xv)::value, false>
-            <<<gr, kThreads, 0, s>>>(g, pass, zc, tgt, Q, x, Wsrc, found, part, nblk, sp);
+        k_trial_rows<1, 4, false, false, 0, TL><<<gr, kThreads, 0, s>>>(g, pass, zc, tgt, Q, x, Wsrc, found, part, nblk, sp);
+      return;
+    }
+    if (side == 1) {  // no x . W product on this side: one instantiation
+      k_trial_fast<1, 4, false, false, TL><<<grid, kThreads, 0, s>>>(g, pass, zc, tgt, Q, x, Wsrc, found, part, nblk);
+      return;
+    }
+    if (trial_mx_ok(g)) {   // side 0 on the matrix cores
+      dim3 gr(nblk, 4, g.H / 128);
+      if (spec && !TL) k_trial_mx<true, false><<<gr, kThreads, 0, s>>>(g, pass, zc, tgt, x, Wsrc, found, part, nblk, sp);
+      else k_trial_mx<false, TL><<<gr, kThreads, 0, s>>>(g, pass, zc, tgt, x, Wsrc, found, part, nblk, sp);
+      return;
+    }
+    if (trial_rows_ok(g)) {
+      dim3 gr(nblk, 4, g.H / 256);
+      with_dp(g, [&](auto dp, auto xv) {
+        if (spec && !TL)
+          k_trial_rows<0, decltype(dp)::value, decltype(xv)::value, true, 0, false>
+              <<<gr, kThreads, 0, s>>>(g, pass, zc, tgt, Q, x, Wsrc, found, part, nblk, sp);
+        else
+          k_trial_rows<0, decltype(dp)::value, decltype(xv)::value, false, 0, TL>
+              <<<gr, kThreads, 0, s>>>(g, pass, zc, tgt, Q, x, Wsrc, found, part, nblk, sp);
+      });
+      return;
+    }
+    const bool ur = (g.H / 4) % 64 == 0;   // one row per wave
+    with_dp(g, [&](auto dp, auto xv) {
+      if (ur)
+        k_trial_fast<0, decltype(dp)::value, decltype(xv)::value, true, TL>
+            <<<grid, kThreads, fast_lds(g), s>>>(g, pass, zc, tgt, Q, x, Wsrc, found, part, nblk);
+      else
+        k_trial_fast<0, decltype(dp)::value, decltype(xv)::value, false, TL>
+            <<<grid, kThreads, fast_lds(g), s>>>(g, pass, zc, tgt, Q, x, Wsrc, found, part, nblk);
     });
-    return;
-  }
-  const bool ur = (g.H / 4) % 64 == 0;   // one row per wave
-  with_dp(g, [&](auto dp, auto xv) {
-    if (ur)
-      k_trial_fast<0, decltype(dp)::value, decltype(xv)::value, true>
-          <<<grid, kThreads, fast_lds(g), s>>>(g, pass, zc, tgt, Q, x, Wsrc, found, part, nblk);
-    else
-      k_trial_fast<0, decltype(dp)::value, decltype(xv)::value, false>
-          <<<grid, kThreads, fast_lds(g), s>>>(g, pass, zc, tgt, Q, x, Wsrc, found, part, nblk);
-  });
+  };
+  if (pass == kTailPass) go(std::integral_constant<bool, true>{});
+  else go(std::integral_constant<bool, false>{});
 }
 
 void launch_select(const Geom& g, const Hyper& hp, const SelectArgs& a, hipStream_t s) {

@@ -16,6 +16,7 @@ constexpr int kPolyHiN = 9;
 constexpr int kTrialSlots = kTrialJ + kPolyN + 2 + kPolyHiN + 1;
 constexpr int kMaxK = 96;        // exponents decided from the polynomial alone go up to this
 constexpr int kMaxPasses = 4;    // => exponents k in [0, 64)
+constexpr int kTailPass = -1;    // trial / select "pass" covering windows 1 .. kMaxPasses - 1 in one launch
 constexpr int kFastD = 16;       // fused weight-stage path for input_size <= 16
 constexpr int kHTCand = 4;       // theta = 0.1, 0.2, 0.4, 0.8 (admm.py:447-480)
 constexpr int kHTSums = 1 + 3 * kHTCand;

@@ -92,7 +92,7 @@ typedef struct AdmmStats {
   int32_t unresolved;         /* weight searches that hit the candidate cap (should be 0) */
   int32_t nonfinite;          /* NaN/Inf seen in line-search sums (should be 0) */
   double direct_frac[8];      /* fraction of elements outside the polynomial regime of each
-                                 weight search (|q| > 2^-8: per-candidate evaluation) */
+                                 weight search (|q| > 2^-5: per-candidate evaluation) */
 } AdmmStats;
 
 typedef struct AdmmCtx AdmmCtx;
@@ -158,9 +158,9 @@ int admm_poll_status(AdmmCtx* ctx, int32_t* unresolved, int32_t* nonfinite);
    admm_profile_read waits for them, returns total ms and launch counts per class, and
    resets.  Classes: */
 enum {
-  ADMM_PROF_SWEEP = 0,        /* k_sweep_t, one launch per time step t */
+  ADMM_PROF_SWEEP = 0,        /* the time sweep: one persistent k_sweep_rows launch (or k_sweep_t per t) */
   ADMM_PROF_TRIAL = 1,        /* first line-search trial pass of the x stage */
-  ADMM_PROF_TRIAL_EXTRA = 2,  /* later trial passes (no-ops once every gate is resolved) */
+  ADMM_PROF_TRIAL_EXTRA = 2,  /* the tail trial pass, windows 1..3 (exits at once when every gate is resolved) */
   ADMM_PROF_ATR_X = 3,        /* G = X^T R (x stage) */
   ADMM_PROF_ATR_H = 4,        /* G = Hprev^T R (h stage) */
   ADMM_PROF_QGEMM_X = 5,      /* Q = X G */

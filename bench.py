@@ -247,6 +247,10 @@ def main():
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--cpu-steps', type=int, default=3, help='timed CPU-baseline steps after step 1 (median)')
     ap.add_argument('--profile-classes', default='sweep,trial,trial_h,trial_extra,atr_x,atr_h,qgemm_x,qgemm_h,resid,small')
+    # rehearsal of the N > 1 path on a one-GPU box: every rank on device 0, torch.distributed over
+    # gloo, so the library stages its all-reduces through the host (not a performance number)
+    ap.add_argument('--dist-backend', default='nccl', choices=['nccl', 'gloo'])
+    ap.add_argument('--one-device', action='store_true', help='all ranks on cuda:0 (rehearsal only)')
     args = ap.parse_args()
 
     world = int(os.environ.get('WORLD_SIZE', '1'))
@@ -254,12 +258,16 @@ def main():
     local_rank = int(os.environ.get('LOCAL_RANK', '0'))
     if world != args.gpus:
         print(f'warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE', file=sys.stderr)
-    torch.cuda.set_device(local_rank)
-    dev = torch.device('cuda', local_rank)
+    dev_index = 0 if args.one_device else local_rank
+    torch.cuda.set_device(dev_index)
+    dev = torch.device('cuda', dev_index)
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group('nccl', device_id=dev)
+        if args.dist_backend == 'nccl':
+            dist.init_process_group('nccl', device_id=dev)
+        else:
+            dist.init_process_group('gloo')
 
     import admm
     from blocks.lstm import LSTM
@@ -317,14 +325,15 @@ def main():
         opt.step()
     barrier()
     elapsed = time.perf_counter() - t0
+    cdev = dev if args.dist_backend == 'nccl' else torch.device('cpu')
     if dist is not None:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed], dtype=torch.float64, device=cdev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     stats = opt.last_step_stats()
     loss = float(torch.nn.functional.mse_loss(model(x), y))
     if dist is not None:
-        lt = torch.tensor([loss * per], dtype=torch.float64, device=dev)
+        lt = torch.tensor([loss * per], dtype=torch.float64, device=cdev)
         dist.all_reduce(lt)
         loss = float(lt.item()) / Bg
 
@@ -375,6 +384,8 @@ def main():
             'value': round(value, 4), 'unit': 'it/s', 'n_gpus': world, 'steps': args.steps, 'warmup': args.warmup,
             'ms_per_step': round(elapsed / args.steps * 1e3, 4), 'higher_is_better': True,
             'scaling': args.scaling, 'vs_baseline': None, 'dtype': 'f32', 'data': 'synthetic',
+            **({'rehearsal': f'{world} ranks on one device over {args.dist_backend} (host-staged all-reduces): '
+                             'not a performance number'} if args.one_device else {}),
             'config': {'workload': f'{args.config.upper()}: ADMMBasedOptimizer.step() ({variant}), '
                                    f'uniform synthetic regression' if gen == 'uniform' else
                                    f'{args.config.upper()}: ADMMBasedOptimizer.step() ({variant}), random-walk windows',

@@ -1,0 +1,59 @@
+"""bench.py's roofline accounting against SURVEY.md 8(d) (CPU).
+
+* survey_terms: the algorithmic flops / bytes per step of SURVEY.md 8(d) -- C3: F = 592.7 GFLOP
+  (446.7 weights + 146.0 sweep), B = 19.9 GB (13.2 + 6.7), t_roof = 3.77 ms; C5 per GPU: see
+  test_survey_terms_c5.  `roofline.frac` is computed from the sweep's B_B (6.73 GB at C3), not from this
+  design's own bytes.
+* roofline_terms('sweep'): the bytes this design moves per sweep launch (DESIGN.md section 4:
+  7.58 GB at C3), which the committed PMC traffic must match (within 2 %).
+"""
+import json
+import os
+
+import pytest
+
+import bench
+
+C3 = (8192, 32, 16, 256)
+C5 = (4096, 64, 1, 512)
+
+
+def test_survey_terms_c3():
+    (fw, bw), (fb, bb) = bench.survey_terms(*C3)
+    assert (fw + fb) / 1e9 == pytest.approx(592.7, abs=0.1)
+    assert fw / 1e9 == pytest.approx(446.7, abs=0.1) and fb / 1e9 == pytest.approx(146.0, abs=0.1)
+    assert (bw + bb) / 1e9 == pytest.approx(19.9, abs=0.05)
+    assert bb == 4.0 * 8192 * 32 * (16 + 25 * 256)          # B_B = 4 B T (D + 25 H)
+    assert bench.step_roofline_s(*C3) * 1e3 == pytest.approx(3.77, abs=0.01)
+
+
+def test_survey_terms_c5():
+    """SURVEY.md 8(d)'s formulas at C5's per-GPU shape give 2 204 GFLOP, 39.2 GB and t_roof = 14.0 ms;
+    the survey quotes 2 285 GFLOP, 39.5 GB and 14.5 ms for the same line (3.7 % / 0.8 % / 3.6 % above
+    its own formulas).  bench.py and DESIGN.md use the formulas."""
+    (fw, bw), (fb, bb) = bench.survey_terms(*C5)
+    assert (fw + fb) / 1e9 == pytest.approx(2204.4, abs=0.1)
+    assert (bw + bb) / 1e9 == pytest.approx(39.2, abs=0.05)
+    assert bench.step_roofline_s(*C5) * 1e3 == pytest.approx(14.0, abs=0.05)
+
+
+def test_sweep_design_bytes_match_pmc(monkeypatch):
+    for k in ('ADMM_LAMH_SKIP', 'ADMM_GX_SWEEP', 'ADMM_SWEEP_ROWS', 'ADMM_TGT_SWEEP'):
+        monkeypatch.delenv(k, raising=False)
+    flops, byts = bench.roofline_terms('sweep', *C3)
+    assert flops == bench.survey_terms(*C3)[1][0]
+    assert byts / 1e9 == pytest.approx(7.58, abs=0.01)
+    traffic = bench.pmc_traffic('sweep', 'c3')     # newest profiles/r*_pmc_c3.json
+    assert traffic is not None
+    assert traffic == pytest.approx(byts, rel=0.02)
+
+
+def test_committed_bench_line_uses_survey_bytes():
+    """The committed round-3 bench line prices the sweep at SURVEY's B_B and reports the whole-step
+    fraction t_roof / t."""
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    d = json.load(open(os.path.join(root, 'profiles', 'r03s_c3_bench.json')))
+    r = d['roofline']
+    assert r['kernel'] == 'sweep' and r['algorithmic_bytes'] == bench.survey_terms(*C3)[1][1]
+    assert r['frac'] == pytest.approx(r['algorithmic_bytes'] / (r['avg_launch_us'] * 1e-6) / 8e12, rel=1e-3)
+    assert d['step_roofline']['step_frac'] == pytest.approx(3.768 / d['ms_per_step'], rel=1e-3)

@@ -136,6 +136,8 @@ struct AdmmCtx {
   // Q in the row-quad layout (k_qgemm3 -> k_trial_rows<1>): 2 = bf16 elements (default), 1 = f32,
   // 0 = row-major f32 (ADMM_QPAIR)
   int qpair = 2;
+  // Q = Hprev G with the G image resident in LDS (k_qgemm_res; ADMM_QRES=0: k_qgemm3)
+  bool qres = true;
   float* gimg = nullptr;   // split image of G_h for k_qgemm3
   hipStream_t sx[kMaxSweepStreams - 1] = {};
   hipEvent_t ev_fork = nullptr, ev_join[kMaxSweepStreams - 1] = {};
@@ -336,7 +338,7 @@ int stage_weights(AdmmCtx* c, int side, hipStream_t s) {
   // 2. trial direction Q = A G (not needed on the fast x side: formed inside the trials)
   if (!(fast && side == 0)) {
     ProfScope ps(c, side == 0 ? ADMM_PROF_QGEMM_X : ADMM_PROF_QGEMM_H, s);
-    if (side == 1 && c->split3) launch_qgemm3(g, c->buf.gates[ADMM_H], c->G, c->gimg, c->Q, s, c->q_pieces, c->qpair);
+    if (side == 1 && c->split3) launch_qgemm3(g, c->buf.gates[ADMM_H], c->G, c->gimg, c->Q, s, c->q_pieces, c->qpair, c->qres);
     else launch_qgemm(g, side, c->buf.x, c->buf.gates[ADMM_H], c->G, c->Q, s);
   }
   // 3. line search: trial passes of kTrialJ exponents each until every gate has passed
@@ -521,6 +523,7 @@ int admm_create(const AdmmDims* dims, const AdmmParams* params, int device, Admm
   if (const char* e = std::getenv("ADMM_SPLIT3")) c->split3 = c->split3 && std::atoi(e) != 0;
   if (const char* e = std::getenv("ADMM_ATR3W")) c->atr3w = std::atoi(e) != 0;
   if (const char* e = std::getenv("ADMM_QPAIR")) c->qpair = std::max(0, std::min(2, std::atoi(e)));
+  if (const char* e = std::getenv("ADMM_QRES")) c->qres = std::atoi(e) != 0;
   if (const char* e = std::getenv("ADMM_Q_PIECES")) c->q_pieces = std::max(1, std::min(3, std::atoi(e)));
   if (const char* e = std::getenv("ADMM_ATR_PIECES")) c->atr_pieces = std::atoi(e) == 2 ? 2 : 3;
   if (const char* e = std::getenv("ADMM_P16")) c->p16 = std::atoi(e) != 0;
@@ -814,12 +817,13 @@ int admm_debug_workspace(AdmmCtx* c, int32_t which, void* dst, int64_t bytes, vo
   if (!c || !dst) return fail(ADMM_EINVAL, "admm_debug_workspace: NULL argument");
   const int64_t need = (int64_t)4 * c->g.BT() * c->g.H * (int64_t)sizeof(float);
   if (bytes < need) return fail(ADMM_EINVAL, "admm_debug_workspace: %lld bytes < %lld", (long long)bytes, (long long)need);
-  const float* src = which == 0 ? c->zc : which == 1 ? c->tgt : nullptr;
+  const float* src = which == 0 ? c->zc : which == 1 ? c->tgt : which == 2 ? c->Q : nullptr;
   if (!src) return fail(ADMM_EINVAL, "admm_debug_workspace: unknown array %d", which);
   DEVICE_GUARD(c->device);
   hipStream_t s = (hipStream_t)stream;
   HIP_TRY(hipMemcpyAsync(dst, src, need, hipMemcpyDeviceToDevice, s));
   HIP_TRY(hipStreamSynchronize(s));
+  if (which == 2) return 1;
   return which == 0 ? (c->z_valid ? 1 : 0) : (c->tgt_valid && c->z_valid ? 1 : 0);
 }
 

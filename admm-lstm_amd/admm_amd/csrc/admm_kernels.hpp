@@ -222,11 +222,14 @@ void launch_atr3(const Geom& g, const float* Sh, const float* zc, const float* t
 // elements (0: row-major f32)
 bool qpair_ok(const Geom& g);
 void launch_qgemm3(const Geom& g, const float* Sh, const float* G, float* gimg, float* Q, hipStream_t s,
-                   int pieces = 3, int qpair = 0);
+                   int pieces = 3, int qpair = 0, bool qres = false);
+// qres: Q = Hprev G with the gate's G image resident in LDS (k_qgemm_res: H = 256, pieces = 1,
+// qpair = 2; bit-identical to k_qgemm3<1, 2>)
+bool qres_ok(const Geom& g);
 // the two halves of launch_qgemm3: G -> split image, then Q = Hprev G (gates with found[q] set skipped)
 void launch_split_g(const Geom& g, const float* G, float* gimg, hipStream_t s);
 void launch_qgemm3_img(const Geom& g, const float* Sh, const float* gimg, float* Q, const int* found, hipStream_t s,
-                       int pieces = 3, int qpair = 0);
+                       int pieces = 3, int qpair = 0, bool qres = false);
 // decide the first passing k in this pass's window; on success update the weights
 struct SelectArgs {
   int side;                 // 0 x, 1 h

@@ -120,6 +120,141 @@ __global__ __launch_bounds__(2 * BM) void k_qgemm3(Geom g, const float* __restri
     }
 }
 
+// ------------------------------------------------------------------ Q = Hprev G, G resident in LDS
+// H = 256 with a one-piece G and bf16 row quads (NP = 1, QP = 2, the default trial direction).
+// k_qgemm3 stages a 128-row tile of Hprev and the whole B image of its gate through LDS for every
+// 16-deep step and waits at two barriers per step pair; its MFMAs ran about a third of the time.
+// Here one workgroup per CU (8 waves, two per SIMD) loads the gate's bf16 G image (piece 0 of
+// k_split_g's image, 128 KB) into LDS once and keeps it for the launch.  Each wave then owns
+// 32-row tiles end to end (32 rows x all 256 columns, eight 32 x 32 accumulators): Hprev goes
+// straight from memory into the A fragment registers (row lane % 32, k = 16c + 8(lane / 32) ..
+// +7), QR_AHEAD steps ahead across tile boundaries, and is split into its two bf16 pieces in
+// registers, so no wave waits on another after the image is in.  The per-accumulator product
+// order (a1 b0, a0 b0 per step, steps in order) is k_qgemm3<1>'s: Q is bit-identical to it.
+// Grid: 32 workgroups per XCD, as 8 row groups x the 4 gates, so the four workgroups that read
+// the same Hprev rows share one L2.
+#ifndef QR_ABL
+#define QR_ABL 0   // timing ablations for tools/kbench (1: no Q stores, 2: no Hprev loads, 4: no MFMAs)
+#endif
+#ifndef QR_AHEAD_SEL
+#define QR_AHEAD_SEL 4
+#endif
+#ifndef QR_STAGGER
+#define QR_STAGGER 0
+#endif
+#ifndef QR_ST_AUX
+#define QR_ST_AUX 2
+#endif
+constexpr int QR_WAVES = 8, QR_AHEAD = QR_AHEAD_SEL;
+__global__ __launch_bounds__(64 * QR_WAVES, 1) void k_qgemm_res(Geom g, const float* __restrict__ Sh,
+                                                                 const bf16x8* __restrict__ gi,
+                                                                 float* __restrict__ Q,
+                                                                 const int* __restrict__ found) {
+  constexpr int H = 256, NK = H / 16, NTT = H / 32;
+  __shared__ bf16x8 Gs[NK * NTT * 64];   // [c][n][lane]: the B fragment of rows 16c.., columns 32n..
+  const int xcd = blockIdx.x % 8, slot = blockIdx.x / 8, q = slot % 4;
+  if (found && found[q]) return;
+  const int ng = gridDim.x / 4, grp = xcd * (gridDim.x / 32) + slot / 4;
+  const bf16x8* gq = gi + (size_t)q * NK * NTT * 192;
+  {   // all 16 units of a thread in flight at once (a load-store loop waits out one L2 trip each)
+    constexpr int NU = NK * NTT * 64 / (64 * QR_WAVES);
+    bf16x8 u[NU];
+#pragma unroll
+    for (int k = 0; k < NU; ++k) {
+      const int i = threadIdx.x + k * 64 * QR_WAVES;
+      u[k] = gq[(i >> 6) * 192 + (i & 63)];
+    }
+#pragma unroll
+    for (int k = 0; k < NU; ++k) Gs[threadIdx.x + k * 64 * QR_WAVES] = u[k];
+  }
+  __syncthreads();
+  const int64_t BT = g.BT(), ntile = (BT + 31) / 32;
+  const int64_t t1 = ntile * (grp + 1) / ng;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, c32 = lane & 31, kh = lane >> 5;
+  int64_t tile = ntile * grp / ng + wave;
+  if (tile >= t1) return;
+  auto rowptr = [&](int64_t tl) {
+    const int64_t r = tl * 32 + c32 < BT ? tl * 32 + c32 : BT - 1;   // rows past BT: computed, not stored
+    return Sh + g.hrow(r) * H + 8 * kh;
+  };
+  const float* ap = rowptr(tile);
+  f32x4 ring[QR_AHEAD][2];
+#pragma unroll
+  for (int s = 0; s < QR_AHEAD; ++s) {
+    ring[s][0] = *reinterpret_cast<const f32x4*>(ap + 16 * s);
+    ring[s][1] = *reinterpret_cast<const f32x4*>(ap + 16 * s + 4);
+    // in slot order: the loop's waits count from the last load of its own order, and a reordered
+    // prologue would make the tile's first step wait for every load and store in flight
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  f32x16 acc[NTT];
+  const __amdgpu_buffer_rsrc_t rQ =
+      __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<__bf16*>(Q) + (int64_t)q * BT * H, 0, (uint32_t)(BT * H * 2), kBufWord3);
+  // the 16 steps of tile `tile` (its rows at ap); the last QR_AHEAD steps load the first rows of
+  // the next tile (at apn)
+  auto steps = [&](const float* apn) {
+#pragma unroll
+    for (int n = 0; n < NTT; ++n) acc[n] = f32x16{};
+#pragma unroll
+    for (int c = 0; c < NK; ++c) {
+      const int sl = c % QR_AHEAD;
+      const f32x8 v = {ring[sl][0].x, ring[sl][0].y, ring[sl][0].z, ring[sl][0].w,
+                       ring[sl][1].x, ring[sl][1].y, ring[sl][1].z, ring[sl][1].w};
+      const float* src = c + QR_AHEAD < NK ? ap + 16 * (c + QR_AHEAD) : apn + 16 * (c + QR_AHEAD - NK);
+      if (QR_ABL & 2) {
+        ring[sl][0] = v.lo + 1.f; ring[sl][1] = v.hi;
+      } else {
+        ring[sl][0] = *reinterpret_cast<const f32x4*>(src);
+        ring[sl][1] = *reinterpret_cast<const f32x4*>(src + 4);
+      }
+      bf16x8 a0, a1;
+      split2(v, a0, a1);
+#pragma unroll
+      for (int n = 0; n < NTT; ++n) {
+        const bf16x8 b0 = Gs[(c * NTT + n) * 64 + lane];
+        if (QR_ABL & 4) {
+          acc[n][0] += (float)a0[0] * (float)b0[0] + (float)a1[1];
+        } else {
+          acc[n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b0, acc[n], 0, 0, 0);
+          acc[n] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b0, acc[n], 0, 0, 0);
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);   // keep each step's loads where they are (hoisted, they spill)
+    }
+  };
+  // Q of tile `tile` as bf16 row quads.  Quads past BT fall outside the descriptor (qres_ok:
+  // BT % 4 == 0), so their stores are dropped without a branch.
+  auto store = [&]() {
+    const uint32_t qo = (uint32_t)((tile * 8 + (lane >> 5)) * H + c32) * 8;   // quad of row acc_row(0, lane)
+#pragma unroll
+    for (int r = 0; r < 16; r += 4)
+#pragma unroll
+      for (int n = 0; n < NTT; ++n) {
+        const f32x4 v = f32x4{acc[n][r], acc[n][r + 1], acc[n][r + 2], acc[n][r + 3]};
+        if (!(QR_ABL & 1) || v[0] == 12345.f)
+        buf_st2<QR_ST_AUX>(rQ, qo + (uint32_t)((r >> 2) * 2 * H + 32 * n) * 8,
+                __builtin_bit_cast(f32x2, __builtin_convertvector(v, bf16x4)));
+      }
+  };
+  // Rotated loop: the steps of the first tile run before it, so the loop is entered in the state
+  // its back edge leaves (the next tile's first loads in flight behind the stores) and the
+  // compiler's waits at the top of the steps count the stores instead of draining them.
+  const float* apn = tile + QR_WAVES < t1 ? rowptr(tile + QR_WAVES) : ap;
+  if (QR_STAGGER && wave >= 4) {
+#pragma unroll
+    for (int i = 0; i < QR_STAGGER; ++i) __builtin_amdgcn_s_sleep(127);
+  }
+  steps(apn);
+  while (true) {
+    store();
+    if (tile + QR_WAVES >= t1) break;
+    tile += QR_WAVES;
+    ap = apn;
+    apn = tile + QR_WAVES < t1 ? rowptr(tile + QR_WAVES) : ap;
+    steps(apn);
+  }
+}
+
 // ------------------------------------------------------------------ slab = Hprev^T R
 // Workgroup: 256 hidden units m x BN columns j of one gate (H % 256 == 0) over the rows of one
 // split, in 16-row steps; 4 waves as 2 (m) x 2 (j) of 128 x BN/2.  BN = 256: 256 accumulators
@@ -535,8 +670,10 @@ void launch_split_g(const Geom& g, const float* G, float* gimg, hipStream_t s) {
 
 bool qpair_ok(const Geom& g) { return g.BT() % 4 == 0; }
 
+bool qres_ok(const Geom& g) { return g.H == 256 && qpair_ok(g) && g.BT() * 256 * 2 < (int64_t)INT32_MAX; }
+
 void launch_qgemm3_img(const Geom& g, const float* Sh, const float* gimg, float* Q, const int* found, hipStream_t s,
-                       int pieces, int qpair) {
+                       int pieces, int qpair, bool qres) {
   // 128-row tiles, two workgroups per CU.  Q3_BM2=256 (8 waves, half the G-image reads per Q row)
   // measured slower at C3: 0.54 against 0.48 ms -- the two independent workgroups of a CU drift
   // out of phase, one staging while the other multiplies, where one workgroup's barriers keep
@@ -546,6 +683,10 @@ void launch_qgemm3_img(const Geom& g, const float* Sh, const float* gimg, float*
 #endif
   const bf16x8* gb = reinterpret_cast<const bf16x8*>(gimg);
   const int qp = qpair_ok(g) ? qpair : 0;
+  if (qres && pieces == 1 && qp == 2 && qres_ok(g)) {   // G resident in LDS: one workgroup per CU
+    k_qgemm_res<<<256, 64 * QR_WAVES, 0, s>>>(g, Sh, gb, Q, found);
+    return;
+  }
   const int BM = pieces == 2 ? Q3_BM2 : 128;   // (pieces 1: 128)
   const int64_t nrt = (g.BT() + BM - 1) / BM;
   dim3 grid((unsigned)(nrt * 4 * (g.H / Q3_BN)));
@@ -561,9 +702,9 @@ void launch_qgemm3_img(const Geom& g, const float* Sh, const float* gimg, float*
 }
 
 void launch_qgemm3(const Geom& g, const float* Sh, const float* G, float* gimg, float* Q, hipStream_t s, int pieces,
-                   int qpair) {
+                   int qpair, bool qres) {
   launch_split_g(g, G, gimg, s);
-  launch_qgemm3_img(g, Sh, gimg, Q, nullptr, s, pieces, qpair);
+  launch_qgemm3_img(g, Sh, gimg, Q, nullptr, s, pieces, qpair, qres);
 }
 
 }  // namespace admm

@@ -185,7 +185,9 @@ int admm_debug_trial(const float* z, const float* tgt, const float* q, int64_t n
 
 /* Test hook (synchronous): copy a workspace array of the context to device memory dst.
    which: 0 = z cache [4][B*T][H], 1 = targets lam/rho + S [4][B*T][H] (valid flag in the
-   return value's sign: 1 if the next x stage will read it, 0 if it will recompute it). */
+   return value's sign: 1 if the next x stage will read it, 0 if it will recompute it),
+   2 = the last h-side trial direction Q = Hprev G_h as stored (layout per ADMM_QPAIR; the
+   first 4*B*T*H*4 bytes of its buffer, returns 1). */
 int admm_debug_workspace(AdmmCtx* ctx, int32_t which, void* dst, int64_t bytes, void* stream);
 
 /* Test hook: while set, every admm_step copies each weight stage's gradient G_q (rho-scaled,

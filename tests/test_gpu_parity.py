@@ -928,6 +928,44 @@ def test_q_bf16_storage_same_trajectory(shape, mods, dev, monkeypatch):
     assert torch.equal(out[0][1], out[1][1])
 
 
+@pytest.mark.parametrize('shape', [(1000, 5, 16, 256), (1001, 4, 3, 256)])
+def test_q_resident_g_bit_identical(shape, mods, dev, monkeypatch):
+    """Q = Hprev G_h with the G image resident in LDS (k_qgemm_res, ADMM_QRES=1, the default at
+    H = 256) against the staged k_qgemm3<1, 2> (ADMM_QRES=0): the same products in the same order,
+    so Q itself (read back through admm_debug_workspace), every exponent and the whole trajectory
+    are bitwise equal.  B*T = 4004 leaves a ragged last 32-row tile."""
+    from blocks.lstm import LSTM
+    from parameters import example_parameter_dictionary
+    from admm_amd import _native as N
+    admm, _ = mods
+    admm.with_dual_y = False
+    B, T, D, H = shape
+    g = torch.Generator().manual_seed(37)
+    x = torch.rand(B, T, D, generator=g).to(dev)
+    y = (0.8 * x.mean((1, 2)).unsqueeze(1) + 0.1 * torch.rand(B, 1, generator=g).to(dev)).contiguous()
+    lib = N.load()
+    out = []
+    for mode in ('0', '1'):
+        monkeypatch.setenv('ADMM_QRES', mode)
+        torch.manual_seed(0)
+        m = LSTM(D, H, 1).to(dev)
+        opt = admm.ADMMBasedOptimizer(m, (x, y), example_parameter_dictionary['GoogleStock'], verbose=False)
+        ks, qs = [], []
+        for _ in range(4):
+            opt.step()
+            ks.append(list(opt.last_step_stats()['k'].values()))
+            buf = torch.empty(4 * B * T * H, dtype=torch.float32, device=dev)
+            assert lib.admm_debug_workspace(opt._ctx, 2, N.ptr(buf), buf.numel() * 4, N.stream_handle(dev)) == 1
+            qs.append(buf[:2 * B * T * H].clone())   # the bf16 row quads: half the f32 buffer
+        out.append((ks, qs, torch.cat([p.detach().flatten() for p in m.parameters()]
+                                      + [v.flatten() for v in opt.gates.values()])))
+        del opt
+    assert out[0][0] == out[1][0]
+    for a, b in zip(out[0][1], out[1][1]):
+        assert torch.equal(a.view(torch.int32), b.view(torch.int32))
+    assert torch.equal(out[0][2], out[1][2])
+
+
 @pytest.mark.parametrize('shape', [(2048, 8, 16, 256), (300, 3, 16, 512)])
 def test_atr_two_piece_split_same_decisions(shape, mods, dev, monkeypatch):
     """The h-side gradient G_h = rho Hprev^T R on two-way bf16 splits (three products, the

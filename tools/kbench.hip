@@ -110,6 +110,18 @@ int main(int argc, char** argv) {
   };
   const std::string mode = argc > 2 ? argv[2] : "";
   if (mode == "s3") { run_s3(); return 0; }
+  if (mode == "q") {   // Q = Hprev G, one-piece G, bf16 row quads: staged k_qgemm3 vs G resident in LDS
+    float* gimg; (void)hipMalloc(&gimg, split3_gimg_floats(g) * 4);
+    float* Q3; (void)hipMalloc(&Q3, (size_t)4 * n * 4);
+    launch_split_g(g, G, gimg, s);
+    const double qb = f4 * BT * g.H + 2.0 * 4 * n, qf = 2.0 * 2 * BT * g.H * 4 * g.H;
+    for (int r = 0; r < 3; ++r) {
+      timeit("qgemm3<1,2>", qb, qf, [&] { launch_qgemm3_img(g, S.p[5], gimg, Q3, nullptr, s, 1, 2, false); });
+      timeit("qgemm_res", qb, qf, [&] { launch_qgemm3_img(g, S.p[5], gimg, Q3, nullptr, s, 1, 2, true); });
+    }
+    timeit("split_g", 0, 0, [&] { launch_split_g(g, G, gimg, s); });
+    return 0;
+  }
   timeit("apply_dwx", 2 * f4 * 4 * n + f4 * BT * g.D, 0, [&] { launch_apply_dwx(g, x, dW, zc, s); });
   timeit("trial_fast side0", f4 * 2 * 4 * n, 0, [&] { launch_trial_fast(g, 0, 0, zc, tgt, nullptr, x, G, found, part, nb, s); });
   timeit("trial_fast side1", f4 * 3 * 4 * n, 0, [&] { launch_trial_fast(g, 1, 0, zc, tgt, Q, x, dW, found, part, nb, s); });

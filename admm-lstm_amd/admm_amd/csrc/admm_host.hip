@@ -548,7 +548,7 @@ int admm_create(const AdmmDims* dims, const AdmmParams* params, int device, Admm
 
   const size_t plane = (size_t)g.BT() * g.H;
   // the sweep's x-stage partials: persistent sweep, fast path, D <= 16, targets from the sweep
-  c->gx_nblk = c->sweep_rows && sweep_rows_gx_ok(g) && fast_path(g) && c->tgt_sweep && c->gx_sweep ? (int)((g.B + 31) / 32) : 0;
+  c->gx_nblk = c->sweep_rows && sweep_rows_gx_ok(g) && fast_path(g) && c->tgt_sweep && c->gx_sweep ? sweep_rows_blocks(g) : 0;
   const int Kmax = g.D > g.H ? g.D : g.H;
   c->nblk_resid = resid_blocks(g);
   c->nblk_trial = std::max(trial_blocks(g), stream_blocks(g) * (trial_mx_ok(g) ? g.H / 128 : trial_rows_ok(g) ? g.H / 256 : 1));

@@ -360,15 +360,26 @@ __global__ __launch_bounds__(kThreads) void k_sweep_wt(int D, int H, int XC, Wei
 // leaves R of its tile in the z tile's LDS slot; two steps later the gate's producer wave folds
 // it in with 16 v_mfma_f32_16x16x4_f32 (K = the tile's 32 rows, M = d, N = 32 columns) into a
 // register ring of NT column tiles that turns once per tile.
+// ROWS = 16 (D == 1): the producer has no registers to spare for that ring, and a one-column x
+// makes the 16x16x4 fold mostly padding, so the consumer forms the partials: each lane takes
+// x_t R_q of its four points for the four gates, a reduce-scatter over the wave's four rows (two
+// xor shuffles) leaves lane (row r, column group) the four-row sum of gate r, which goes to an
+// LDS slot of the tile (by step parity).  One step later, past the barrier, thread (wave q, lane
+// j) adds the four waves' sums of gate q, column j of that tile in wave order into a register
+// ring of the NT column tiles, and writes its slab entries at the end: a fixed summation order,
+// 8 KB of LDS and NT registers.
 template <int NT, int XC, bool GX, int ROWS = 32>
 __global__ __launch_bounds__(SR_THREADS) void k_sweep_rows(Geom g, const bf16x8* __restrict__ wt, Hyper hp,
                                                             SweepT a) {
   using SG = SrGeom<NT, XC, ROWS>;
-  static_assert(ROWS == 32 || !GX, "the G_x fold is built for 32-row tiles");
+  constexpr bool GXP = GX && ROWS == 32;   // G_x partials folded by the producer (MFMA)
+  constexpr bool GXC = GX && ROWS == 16;   // ... accumulated by the consumer (D == 1)
   constexpr int H = SG::H, XK = SG::XK, K2 = SG::K2, KC2 = SG::KC2, AST = SG::AST, AP = SG::APIECE;
   constexpr int TW = SG::TW, ZG = ROWS * TW;   // tile width; one gate's z tile (floats)
   __shared__ __attribute__((aligned(16))) __bf16 Ab[2][3 * AP];
   __shared__ __attribute__((aligned(16))) float Zb[2][4 * ZG];
+  // GXC: per step parity, consumer wave and gate, the four-row sums of the tile's TW columns
+  __shared__ __attribute__((aligned(16))) float Px[GXC ? 2 : 1][GXC ? 4 : 1][GXC ? 4 : 1][GXC ? TW : 1];
   const int T = g.T, D = g.D;
   const int64_t m0 = a.r0 + (int64_t)blockIdx.x * ROWS;
   const int64_t rs = (int64_t)(T + 1) * H;
@@ -624,6 +635,15 @@ __global__ __launch_bounds__(SR_THREADS) void k_sweep_rows(Geom g, const bf16x8*
   f32x4 cring[NT];
 #pragma unroll
   for (int k = 0; k < NT; ++k) cring[k] = f32x4{};
+  // GXC: this thread's slab entries (gate = its consumer wave, column = its lane) of each column
+  // tile, a ring turned once per step like cring
+  float gxr[GXC ? NT : 1];   // slot 0 = the tile summed next (turned once per step)
+#pragma unroll
+  for (int k = 0; k < (GXC ? NT : 1); ++k) gxr[k] = 0.f;
+  const int cq = ct >> 6;     // GXC: the gate this thread sums (its consumer wave)
+  // the slot read at step 0 holds no tile: zeros (the ring turns for it like for any step)
+  if (GXC) *reinterpret_cast<f32x4*>(&Px[GXC ? 1 : 0][0][0][0] + 4 * ct) = f32x4{};
+  const int64_t bx = min(m0 + row, a.r1 - 1);
   St4 nxt;
   load_tile(1, 0, nxt);
   load_x(2);                 // step 0: the producer computes tile (1, 0)
@@ -638,6 +658,7 @@ __global__ __launch_bounds__(SR_THREADS) void k_sweep_rows(Geom g, const bf16x8*
       const unsigned long long ta_ = clock64();
 #endif
       const St4 cur = nxt;
+      const float xm = GXC && rok ? a.x[bx * T + (t - 1)] : 0.f;   // GXC (D == 1): x_t of this row
 #ifdef SR_TIMING
       asm volatile("" :: "v"(cur.f0), "v"(cur.g0), "v"(cur.c0), "v"(cur.h0), "v"(cur.li), "v"(cur.lf), "v"(cur.lg),
                    "v"(cur.lo), "v"(cur.lc), "v"(cur.lh), "v"(cur.cp));
@@ -676,12 +697,39 @@ __global__ __launch_bounds__(SR_THREADS) void k_sweep_rows(Geom g, const bf16x8*
         ti = tgt_quot(li, hp.rho[0], i1); tf = tgt_quot(lf, hp.rho[1], f1);
         tg = tgt_quot(lg, hp.rho[2], g1); to = tgt_quot(lo, hp.rho[3], o1);
       }
-      if constexpr (GX) {   // R = (phi(z) - tgt) phi'(z) into the z slot (0 past the last row)
+      if constexpr (GXP) {   // R = (phi(z) - tgt) phi'(z) into the z slot (0 past the last row)
         const float m = rok ? 1.f : 0.f;
         Z[0] = (ai - ti) * di * m;
         Z[ZG4] = (af - tf) * df * m;
         Z[2 * ZG4] = (ag - tg) * dg * m;
         Z[3 * ZG4] = (ao - to) * dO * m;
+      }
+      if constexpr (GXC) {   // x_t R_q of the four points (0 past the last row: xm = 0)
+        const int sp = ((t - 1) * NT + n) & 1;
+        const bool b1 = (lane >> 5) & 1, b0 = (lane >> 4) & 1;   // the row's bits within the wave
+        // rows r and r ^ 2 (lanes 32 apart): keep gates 2 b1, 2 b1 + 1; then rows r, r ^ 1: keep r.
+        // One gate pair at a time (registers).
+        auto pair = [&](f32x4 va, f32x4 vb) {   // gates q, q + 2 -> the kept one, summed over r, r ^ 2
+          f32x4 k = b1 ? vb : va;
+          const f32x4 sx = b1 ? va : vb;
+#pragma unroll
+          for (int u = 0; u < 4; ++u) k[u] += __shfl_xor(sx[u], 32, 64);
+          return k;
+        };
+        const f32x4 k0 = pair((ai - ti) * di * xm, (ag - tg) * dg * xm);
+        const f32x4 k1 = pair((af - tf) * df * xm, (ao - to) * dO * xm);
+        f32x4 kk = b0 ? k1 : k0;
+        const f32x4 sk = b0 ? k0 : k1;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) kk[u] += __shfl_xor(sk[u], 16, 64);
+        *reinterpret_cast<f32x4*>(&Px[sp][cq][lane >> 4][j4]) = kk;
+        // the previous step's tile: gate cq, column lane, summed over the four waves in order
+        const float* pp = &Px[sp ^ 1][0][cq][lane];
+        const float tot = ((pp[0] + pp[4 * TW]) + pp[8 * TW]) + pp[12 * TW];
+        const float h0 = gxr[0] + tot;
+#pragma unroll
+        for (int k = 0; k + 1 < NT; ++k) gxr[k] = gxr[k + 1];
+        gxr[NT - 1] = h0;
       }
 #ifdef SR_TIMING
       asm volatile("" :: "v"(i1), "v"(f1), "v"(g1), "v"(o1), "v"(c1), "v"(h1), "v"(li), "v"(lf), "v"(lg), "v"(lo), "v"(lc));
@@ -721,6 +769,17 @@ __global__ __launch_bounds__(SR_THREADS) void k_sweep_rows(Geom g, const bf16x8*
       }
       SR_SYNC();             // end of step
     }
+  }
+  if constexpr (GXC) {   // past the last step's barrier: its tile, then the slab (D == 1)
+    const float* pp = &Px[((T - 1) * NT + NT - 1) & 1][0][cq][lane];
+    const float tot = ((pp[0] + pp[4 * TW]) + pp[8 * TW]) + pp[12 * TW];
+    const float h0 = gxr[0] + tot;
+#pragma unroll
+    for (int k = 0; k + 1 < NT; ++k) gxr[k] = gxr[k + 1];
+    gxr[NT - 1] = h0;
+    float* out = a.gx_slab + ((int64_t)blockIdx.x * 4 + cq) * H + lane;
+#pragma unroll
+    for (int k = 0; k < NT; ++k) out[TW * k] = gxr[k];   // slot k = column tile k after T NT + 1 turns
   }
 #ifdef SR_TIMING
   if (threadIdx.x == 256) {
@@ -2832,7 +2891,8 @@ bool sweep_rows_ok(const Geom& g) {
          4 * g.BT() * g.H * 4 < (int64_t)UINT32_MAX;   // the 4-plane z cache / target descriptors
 }
 
-bool sweep_rows_gx_ok(const Geom& g) { return sweep_rows_ok(g) && !sweep_r16(g) && g.D <= 16; }
+bool sweep_rows_gx_ok(const Geom& g) { return sweep_rows_ok(g) && (sweep_r16(g) ? g.D == 1 : g.D <= 16); }
+int sweep_rows_blocks(const Geom& g) { return (int)((g.B + (sweep_r16(g) ? 15 : 31)) / (sweep_r16(g) ? 16 : 32)); }
 
 static int sweep_xc(const Geom& g) { return sweep_r16(g) ? (g.D + 31) / 32 : (g.D + 15) / 16; }
 
@@ -2858,7 +2918,10 @@ static void launch_sweep_rows_xc(const Geom& g, const bf16x8* wt, const Hyper& h
   if (sweep_r16(g)) {
     dim3 grid(cdiv64(a.r1 - a.r0, 16));
     switch (g.H / 64) {
-#define SR16_CASE(N) case N: k_sweep_rows<N, XC, false, 16><<<grid, SR_THREADS, 0, s>>>(g, wt, hp, a); break;
+#define SR16_CASE(N) case N: \
+  if (XC == 1 && g.D == 1 && a.gx_slab) k_sweep_rows<N, XC, true, 16><<<grid, SR_THREADS, 0, s>>>(g, wt, hp, a); \
+  else k_sweep_rows<N, XC, false, 16><<<grid, SR_THREADS, 0, s>>>(g, wt, hp, a); \
+  break;
       SR16_CASE(5) SR16_CASE(6) SR16_CASE(7) SR16_CASE(8)
 #undef SR16_CASE
       default: break;

@@ -112,7 +112,8 @@ void launch_sweep_t(const Geom& g, int t, const Weights& w, const Hyper& hp, con
 // Whole sweep in one persistent launch (k_sweep_rows): eligible when sweep_rows_ok(g).
 // wt: sweep_wt_floats(g) floats, filled by launch_sweep_wt from the current weights.
 bool sweep_rows_ok(const Geom& g);
-bool sweep_rows_gx_ok(const Geom& g);   // ... and it can form the x stage's G_x partials (32-row tiles, D <= 16)
+bool sweep_rows_gx_ok(const Geom& g);   // ... and it can form the x stage's G_x partials (32-row tiles with D <= 16, 16-row tiles with D == 1)
+int sweep_rows_blocks(const Geom& g);   // its workgroups = its G_x slabs
 size_t sweep_wt_floats(const Geom& g);
 void launch_sweep_wt(const Geom& g, const Weights& w, float* wt, hipStream_t s);
 void launch_sweep_rows(const Geom& g, const float* wt, const Hyper& hp, const SweepT& a, hipStream_t s);

@@ -793,12 +793,15 @@ def test_speculative_x_update_bit_identical(shape, D_, mods, dev, monkeypatch):
     assert torch.equal(out[0][2], out[1][2])
 
 
-@pytest.mark.parametrize('shape,D_', [((300, 3, 256), 16), ((200, 5, 64), 5), ((8192, 8, 256), 16)])
+@pytest.mark.parametrize('shape,D_', [((300, 3, 256), 16), ((200, 5, 64), 5), ((8192, 8, 256), 16),
+                                      ((300, 4, 512), 1), ((200, 3, 320), 1)])
 def test_sweep_gx_matches_resid_pass(shape, D_, mods, dev, monkeypatch):
-    """k_sweep_rows<GX> forms the next x stage's X^T R partials with f32 MFMAs from the new
-    state (default); ADMM_GX_SWEEP=0 runs k_resid_gx over z and tgt instead.  Same products,
-    another summation order: identical line-search exponents, weights and state within fp32
-    rounding (1e-5), over several steps.  B % 32 != 0 covers the ragged last row block."""
+    """k_sweep_rows<GX> forms the next x stage's X^T R partials from the new state (default):
+    with f32 MFMAs in the producer for 32-row tiles, and in the consumer (shuffle reduce-scatter,
+    LDS step slots) for the 16-row tiles of 256 < H <= 512 with D = 1; ADMM_GX_SWEEP=0 runs
+    k_resid_gx over z and tgt instead.  Same products, another summation order: identical
+    line-search exponents, weights and state within fp32 rounding (1e-5), over several steps.
+    B % 32 != 0 and B % 16 != 0 cover the ragged last row block."""
     from blocks.lstm import LSTM
     from parameters import example_parameter_dictionary
     admm, _ = mods

@@ -139,12 +139,6 @@ __global__ __launch_bounds__(2 * BM) void k_qgemm3(Geom g, const float* __restri
 #ifndef QR_AHEAD_SEL
 #define QR_AHEAD_SEL 4
 #endif
-#ifndef QR_STAGGER
-#define QR_STAGGER 0
-#endif
-#ifndef QR_ST_AUX
-#define QR_ST_AUX 2
-#endif
 constexpr int QR_WAVES = 8, QR_AHEAD = QR_AHEAD_SEL;
 __global__ __launch_bounds__(64 * QR_WAVES, 1) void k_qgemm_res(Geom g, const float* __restrict__ Sh,
                                                                  const bf16x8* __restrict__ gi,
@@ -232,7 +226,7 @@ __global__ __launch_bounds__(64 * QR_WAVES, 1) void k_qgemm_res(Geom g, const fl
       for (int n = 0; n < NTT; ++n) {
         const f32x4 v = f32x4{acc[n][r], acc[n][r + 1], acc[n][r + 2], acc[n][r + 3]};
         if (!(QR_ABL & 1) || v[0] == 12345.f)
-        buf_st2<QR_ST_AUX>(rQ, qo + (uint32_t)((r >> 2) * 2 * H + 32 * n) * 8,
+        buf_st2(rQ, qo + (uint32_t)((r >> 2) * 2 * H + 32 * n) * 8,
                 __builtin_bit_cast(f32x2, __builtin_convertvector(v, bf16x4)));
       }
   };
@@ -240,10 +234,6 @@ __global__ __launch_bounds__(64 * QR_WAVES, 1) void k_qgemm_res(Geom g, const fl
   // its back edge leaves (the next tile's first loads in flight behind the stores) and the
   // compiler's waits at the top of the steps count the stores instead of draining them.
   const float* apn = tile + QR_WAVES < t1 ? rowptr(tile + QR_WAVES) : ap;
-  if (QR_STAGGER && wave >= 4) {
-#pragma unroll
-    for (int i = 0; i < QR_STAGGER; ++i) __builtin_amdgcn_s_sleep(127);
-  }
   steps(apn);
   while (true) {
     store();

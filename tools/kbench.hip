@@ -8,6 +8,8 @@
 #include <vector>
 #include <string>
 #include <cmath>
+#include <cstring>
+#include <cstdint>
 #include <algorithm>
 #include "../admm-lstm_amd/admm_amd/csrc/admm_kernels.hpp"
 
@@ -120,6 +122,22 @@ int main(int argc, char** argv) {
       timeit("qgemm_res", qb, qf, [&] { launch_qgemm3_img(g, S.p[5], gimg, Q3, nullptr, s, 1, 2, true); });
     }
     timeit("split_g", 0, 0, [&] { launch_split_g(g, G, gimg, s); });
+    {   // Q of the two kernels (bf16 row quads): identical unless the k order differs (QR_KPERM)
+      float* Q4; (void)hipMalloc(&Q4, (size_t)4 * n * 4);
+      launch_qgemm3_img(g, S.p[5], gimg, Q3, nullptr, s, 1, 2, false);
+      launch_qgemm3_img(g, S.p[5], gimg, Q4, nullptr, s, 1, 2, true);
+      (void)hipDeviceSynchronize();
+      std::vector<uint16_t> a(2 * n * 4 / 2), b(a.size());
+      (void)hipMemcpy(a.data(), Q3, a.size() * 2, hipMemcpyDeviceToHost);
+      (void)hipMemcpy(b.data(), Q4, b.size() * 2, hipMemcpyDeviceToHost);
+      auto f = [](uint16_t h) { uint32_t u = (uint32_t)h << 16; float x; memcpy(&x, &u, 4); return x; };
+      double md = 0, mx = 0; size_t neq = 0;
+      for (size_t i = 0; i < a.size(); ++i) {
+        md = std::max(md, (double)std::fabs(f(a[i]) - f(b[i]))); mx = std::max(mx, (double)std::fabs(f(a[i])));
+        neq += a[i] != b[i];
+      }
+      printf("qgemm_res vs qgemm3: %zu of %zu bf16 differ, max |diff| %.3e (max |Q| %.3e)\n", neq, a.size(), md, mx);
+    }
     return 0;
   }
   timeit("apply_dwx", 2 * f4 * 4 * n + f4 * BT * g.D, 0, [&] { launch_apply_dwx(g, x, dW, zc, s); });

@@ -46,6 +46,9 @@ static void timeit(const char* name, double bytes, double flops, const std::func
 
 int main(int argc, char** argv) {
   Geom g{8192, 8192, 32, 16, 256, 1};
+  if (argc > 3) g.T = atoi(argv[3]);
+  if (argc > 4) g.D = atoi(argv[4]);
+  if (argc > 5) g.H = atoi(argv[5]);
   g.set_T();
   if (argc > 1) g.B = g.Bg = atoll(argv[1]);
   const int64_t BT = g.BT(), n = BT * g.H, P = g.B * (int64_t)g.TP() * g.H;

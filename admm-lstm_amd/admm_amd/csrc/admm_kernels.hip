@@ -1920,8 +1920,11 @@ __device__ __forceinline__ void trial_rows_body(const Geom& g, int q, int pass, 
   dq_run<TANH>(dq, acc, true);
 }
 
+#ifndef TR_MINB
+#define TR_MINB 1   // workgroups per CU the register allocation must allow
+#endif
 template <int SIDE, int DP, bool XV, bool SPEC, int QP = 0, bool TAIL = false>
-__global__ __launch_bounds__(kThreads) void k_trial_rows(Geom g, int pass, const float* __restrict__ zc,
+__global__ __launch_bounds__(kThreads, TR_MINB) void k_trial_rows(Geom g, int pass, const float* __restrict__ zc,
                                                          const float* __restrict__ tgt, const float* __restrict__ Q,
                                                          const float* __restrict__ x, const float* __restrict__ Gx,
                                                          const int* __restrict__ found, double* __restrict__ part,

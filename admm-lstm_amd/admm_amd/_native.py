@@ -80,6 +80,7 @@ _SIGNATURES = {
     'admm_profile_read': (c_int, [c_void_p, POINTER(c_double), POINTER(c_int32)]),
     'admm_debug_workspace': (c_int, [c_void_p, c_int32, c_void_p, c_int64, c_void_p]),
     'admm_debug_trace': (c_int, [c_void_p, c_void_p, c_void_p]),
+    'admm_debug_trace_resid': (c_int, [c_void_p, c_void_p, c_void_p]),
     'admm_debug_force': (c_int, [c_void_p, c_void_p, c_int32]),
     'admm_debug_own': (c_int, [c_void_p, c_void_p, POINTER(c_float)]),
     'admm_debug_trial': (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_int32, c_int32, POINTER(c_double),

@@ -125,10 +125,18 @@ struct AdmmCtx {
   // f32-accurate (ADMM_Q_PIECES).  Q only enters the line-search increments (DESIGN.md "trial
   // direction precision"); G itself, which updates the weights, is not rounded.
   int q_pieces = 1;
-  // split pieces of the h-side gradient G_h = rho Hprev^T R (k_atr3w): 2 = the three products of
-  // two-way splits, ~2^-16 relative per product -- the accuracy of the reference's own fp32 sums of
-  // B*T terms (DESIGN.md "h-side gradient on two-way splits"); ADMM_ATR_PIECES=3: f32-accurate split3
-  int atr_pieces = 2;
+  // split pieces of the h-side gradient G_h = rho Hprev^T R (k_atr3w): 3 = split3's six products,
+  // f32-accurate (tests/test_gpu_weight_phase.py: within the error of an fp32 GEMM of the same
+  // operands); ADMM_ATR_PIECES=2: two-way bf16 splits, ~2^-16 relative per product, which measured
+  // 1.3-3.7x a torch fp32 GEMM's error on perturbed states -- not f32-equivalent
+  int atr_pieces = 3;
+  // ... unless the operand ranges are known: the h-side gradient then runs on scaled fp16 two-way
+  // splits (k_atr3w<2, true>: f32-accurate at the matrix work of two pieces; ADMM_ATR_F16=0: off).
+  // range [8] (device): SweepT::range's maxima from the last persistent sweep ([0..4], valid when
+  // range_valid) and max_row sum_d |x_d| ([5], valid when x1_valid)
+  bool atr_f16 = true;
+  float* range = nullptr;
+  bool range_valid = false, x1_valid = false;
   // pass 0 of a gate whose last exponent was past the first window also sums the per-candidate
   // elements' polynomial, so the exponents past it are decided without pass 1 (ADMM_P16=0: off)
   bool p16 = true;
@@ -165,6 +173,8 @@ struct AdmmCtx {
   std::vector<std::pair<int, std::pair<hipEvent_t, hipEvent_t>>> ev_used;
   // admm_debug_trace: caller buffers receiving each stage's G (tests)
   float* trace_g[2] = {nullptr, nullptr};
+  // admm_debug_trace_resid: caller buffers receiving each stage's residual R [4][BT][H] (tests)
+  float* trace_r[2] = {nullptr, nullptr};
   // admm_debug_force: forced line-search decisions [8 exponents, h_T failing tests] (tests)
   int* force_dev = nullptr;
   bool force_on = false;
@@ -297,8 +307,16 @@ int stage_weights(AdmmCtx* c, int side, hipStream_t s) {
     launch_resid_gx(g, c->hp, c->buf.x, S, L, c->zc, c->tgt, c->gslab, ns, c->tgt_valid && c->z_valid, s);
   } else if (fast && c->split3) {
     ns = atr3_splits(g);
+    // scaled fp16 operands once a persistent sweep has left the operand ranges of this state
+    const bool f16 = c->atr_f16 && c->range_valid && c->atr3w && atr3w_ok(g);
+    if (f16 && !c->x1_valid) {
+      HIP_TRY(hipMemsetAsync(c->range + 5, 0, sizeof(float), s));
+      launch_x_l1max(g, c->buf.x, c->range, s);
+      c->x1_valid = true;
+    }
     ProfScope ps(c, ADMM_PROF_ATR_H, s);
-    launch_atr3(g, c->buf.gates[ADMM_H], zh, c->tgt, c->gslab, ns, s, c->atr3w, c->atr_pieces);
+    launch_atr3(g, c->buf.gates[ADMM_H], zh, c->tgt, c->gslab, ns, s, c->atr3w, c->atr_pieces,
+                f16 ? c->range : nullptr, f16 ? c->dW : nullptr);
   } else if (fast) {
     ns = atr_splits(g, 1);
     ProfScope ps(c, ADMM_PROF_ATR_H, s);
@@ -322,8 +340,14 @@ int stage_weights(AdmmCtx* c, int side, hipStream_t s) {
     ProfScope ps(c, side == 0 ? ADMM_PROF_ATR_X : ADMM_PROF_ATR_H, s);
     launch_atr(g, side, c->buf.x, c->buf.gates[ADMM_H], c->R, c->gslab, ns, s);
   }
+  if (c->trace_r[side]) {   // the residual this stage's G was formed from, as that kernel formed it
+    if (!fast) HIP_TRY(hipMemcpyAsync(c->trace_r[side], c->R, (size_t)4 * g.BT() * g.H * sizeof(float),
+                                      hipMemcpyDeviceToDevice, s));
+    else if (side == 0) launch_debug_resid(g, gsrc == c->gx_slab ? 0 : 1, c->zc, c->tgt, c->trace_r[0], s);
+    else launch_debug_resid(g, 2, zh, c->tgt, c->trace_r[1], s);
+  }
   launch_reduce_g(g, side, c->hp, gsrc, ns, c->G, c->found, spec && side == 0 ? c->kpred : nullptr, c->stats, s,
-                  c->p16);
+                  c->p16, side == 1 ? c->range : nullptr);   // (the h side clears the ranges for the sweep)
   // (x stage with G_y pending: one all-reduce for both, then the wy update)
   const bool with_gy = side == 0 && c->gy_pending;
   int rc = allreduce_f32(c, c->G, (size_t)4 * Kd * g.H + (with_gy ? (size_t)g.H * g.O : 0), s);
@@ -418,6 +442,7 @@ int stage_sweep(AdmmCtx* c, hipStream_t s) {
       c->lamh_known = true;
     }
     sa.lamh_nz = c->lamh_known && c->lamh_skip ? c->lamh_nz : nullptr;
+    sa.range = c->range;   // zeroed by this step's h-stage k_reduce_g
     launch_sweep_wt(g, w, c->swt, s);
     launch_sweep_rows(g, c->swt, c->hp, sa, s);
   } else {
@@ -527,6 +552,7 @@ int admm_create(const AdmmDims* dims, const AdmmParams* params, int device, Admm
   if (const char* e = std::getenv("ADMM_Q_PIECES")) c->q_pieces = std::max(1, std::min(3, std::atoi(e)));
   if (const char* e = std::getenv("ADMM_ATR_PIECES")) c->atr_pieces = std::atoi(e) == 2 ? 2 : 3;
   if (const char* e = std::getenv("ADMM_P16")) c->p16 = std::atoi(e) != 0;
+  if (const char* e = std::getenv("ADMM_ATR_F16")) c->atr_f16 = std::atoi(e) != 0;
   Hyper& h = c->hp;
   for (int i = 0; i < 7; ++i) h.rho[i] = params->rho[i];
   h.rinv_exact = 1;
@@ -568,7 +594,7 @@ int admm_create(const AdmmDims* dims, const AdmmParams* params, int device, Admm
       (rc = dalloc(&c->found, 12)) || (rc = dalloc(&c->pick, 4)) ||
       (rc = dalloc(&c->U, (size_t)g.B * g.O)) || (rc = dalloc(&c->wy_slab, (size_t)c->wy_nsplit * g.H * g.O)) ||
       (rc = dalloc(&c->Gy, (size_t)g.H * g.O)) || (rc = dalloc(&c->ht_part, (size_t)c->ht_nblk * kHTSums)) ||
-      (rc = dalloc(&c->ht_sums, kHTSums)) || (rc = dalloc(&c->stats, 1)) || (rc = dalloc(&c->lamh_nz, 1)) || (rc = dalloc(&c->force_dev, 9)) ||
+      (rc = dalloc(&c->ht_sums, kHTSums)) || (rc = dalloc(&c->stats, 1)) || (rc = dalloc(&c->lamh_nz, 1)) || (rc = dalloc(&c->force_dev, 9)) || (rc = dalloc(&c->range, 8)) ||
       (c->sweep_rows && (rc = dalloc(&c->swt, sweep_wt_floats(g)))) ||
       (c->split3 && (rc = dalloc(&c->gimg, split3_gimg_floats(g)))) ||
       (c->spec_x && ((rc = dalloc(&c->zx, 4 * plane)) || (rc = dalloc(&c->kpred, 4)))) ||
@@ -585,7 +611,7 @@ int admm_create(const AdmmDims* dims, const AdmmParams* params, int device, Admm
     admm_destroy(c);
     return fail(ADMM_EHIP, "stream/event creation failed");
   }
-  if (hipMemset(c->stats, 0, sizeof(DevStats)) != hipSuccess) {
+  if (hipMemset(c->stats, 0, sizeof(DevStats)) != hipSuccess || hipMemset(c->range, 0, 8 * sizeof(float)) != hipSuccess) {
     admm_destroy(c);
     return fail(ADMM_EHIP, "hipMemset(stats) failed");
   }
@@ -603,7 +629,7 @@ int admm_destroy(AdmmCtx* c) {
   if (!c) return ADMM_OK;
   DeviceGuard dg_(c->device);
   void* ptrs[] = {c->zc, c->tgt, c->R, c->Q, c->G, c->dW, c->gslab, c->tr_part, c->tr_sums, c->tr_poly, c->found, c->pick,
-                  c->U, c->wy_slab, c->Gy, c->ht_part, c->ht_sums, c->stats, c->swt, c->gimg, c->zx, c->kpred, c->gx_slab, c->lamh_nz, c->force_dev};
+                  c->U, c->wy_slab, c->Gy, c->ht_part, c->ht_sums, c->stats, c->swt, c->gimg, c->zx, c->kpred, c->gx_slab, c->lamh_nz, c->force_dev, c->range};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   if (c->comm) ncclCommDestroy(c->comm);
@@ -637,6 +663,7 @@ int admm_bind(AdmmCtx* c, const AdmmBuffers* b) {
   c->tgt_valid = false;
   c->gx_valid = false;
   c->lamh_known = false;
+  c->range_valid = c->x1_valid = false;
   return ADMM_OK;
 }
 
@@ -652,6 +679,7 @@ int admm_invalidate_cache(AdmmCtx* c) {
   c->tgt_valid = false;
   c->gx_valid = false;
   c->lamh_known = false;
+  c->range_valid = c->x1_valid = false;
   return ADMM_OK;
 }
 
@@ -690,6 +718,7 @@ int admm_init_state(AdmmCtx* c, void* stream) {
   c->z_valid = true;
   c->tgt_valid = false;   // recomputed from the new state by the first x stage
   c->gx_valid = false;
+  c->range_valid = false;   // the first h stage takes split3 (no sweep has bounded its operands)
   HIP_TRY(hipMemsetAsync(c->lamh_nz, 0, sizeof(int), s));   // the duals were just zeroed
   c->lamh_known = true;
   return ADMM_OK;
@@ -713,6 +742,7 @@ int admm_step(AdmmCtx* c, void* stream) {
   c->z_valid = true;  // the sweep left x_t Wx + h_{t-1} Wh of the final state in the cache
   c->tgt_valid = c->sweep_rows && fast_path(c->g) && c->tgt_sweep;
   c->gx_valid = c->tgt_valid && c->gx_slab != nullptr;
+  c->range_valid = c->sweep_rows;   // the persistent sweep tracked the next weight phase's operand ranges
   c->steps++;
   return ADMM_OK;
 }
@@ -831,6 +861,13 @@ int admm_debug_trace(AdmmCtx* c, float* gx, float* gh) {
   if (!c) return fail(ADMM_EINVAL, "NULL ctx");
   c->trace_g[0] = gx;
   c->trace_g[1] = gh;
+  return ADMM_OK;
+}
+
+int admm_debug_trace_resid(AdmmCtx* c, float* rx, float* rh) {
+  if (!c) return fail(ADMM_EINVAL, "NULL ctx");
+  c->trace_r[0] = rx;
+  c->trace_r[1] = rh;
   return ADMM_OK;
 }
 

@@ -283,6 +283,14 @@ __global__ __launch_bounds__(kThreads) void k_sweep_t(Geom g, int t, Weights w, 
 // t boundary the producer's tile (t+1, 0) needs h_t of the tile the consumer is finishing:
 // it runs K up to that tile's 32 columns, meets the consumer at a mid-step barrier, then
 // finishes the last two chunks.
+// max over the wave of a non-negative v, folded into *dst (float bits, atomicMax: for values >= 0
+// the integer order of the bits is the float order) by lane 0 -- a vector atomic
+__device__ __forceinline__ void range_max(float* dst, float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, kWave));
+  if ((threadIdx.x & 63) == 0) atomicMax(reinterpret_cast<unsigned*>(dst), __float_as_uint(v));
+}
+
 constexpr int SR_ROWS = 32, SR_THREADS = 512;
 #ifdef SR_TIMING
 __device__ unsigned long long g_sr_wait[2048][2];   // per workgroup: cycles the producer / consumer wave 0 waited at barriers
@@ -380,6 +388,7 @@ __global__ __launch_bounds__(SR_THREADS) void k_sweep_rows(Geom g, const bf16x8*
   __shared__ __attribute__((aligned(16))) float Zb[2][4 * ZG];
   // GXC: per step parity, consumer wave and gate, the four-row sums of the tile's TW columns
   __shared__ __attribute__((aligned(16))) float Px[GXC ? 2 : 1][GXC ? 4 : 1][GXC ? 4 : 1][GXC ? TW : 1];
+  __shared__ float Rg[GXC ? 5 * 256 : 1];   // GXC: the consumer threads' running range maxima
   const int T = g.T, D = g.D;
   const int64_t m0 = a.r0 + (int64_t)blockIdx.x * ROWS;
   const int64_t rs = (int64_t)(T + 1) * H;
@@ -396,11 +405,15 @@ __global__ __launch_bounds__(SR_THREADS) void k_sweep_rows(Geom g, const bf16x8*
   };
 
   // A image for t = 1: [x_1 | h_0]
+  float mh0 = 0.f;   // max |h_0| of the block's rows (range[4])
   for (int i = threadIdx.x; i < ROWS * K2; i += SR_THREADS) {
     const int row = i / K2, k = i % K2;
     const int64_t b = min(m0 + row, a.r1 - 1);
-    put_a(1, row, k, k < XK ? (k < D ? a.x[b * T * D + k] : 0.f) : a.S.p[5][b * rs + (k - XK)]);
+    const float v = k < XK ? (k < D ? a.x[b * T * D + k] : 0.f) : a.S.p[5][b * rs + (k - XK)];
+    if (k >= XK) mh0 = fmaxf(mh0, fabsf(v));
+    put_a(1, row, k, v);
   }
+  if (a.range) range_max(a.range + 4, mh0);
   __syncthreads();
 
   if (ROWS == 16 && wave < 4) {
@@ -644,6 +657,14 @@ __global__ __launch_bounds__(SR_THREADS) void k_sweep_rows(Geom g, const bf16x8*
   // the slot read at step 0 holds no tile: zeros (the ring turns for it like for any step)
   if (GXC) *reinterpret_cast<f32x4*>(&Px[GXC ? 1 : 0][0][0][0] + 4 * ct) = f32x4{};
   const int64_t bx = min(m0 + row, a.r1 - 1);
+  // range (a.range): max |phi(z) - tgt| per gate and max |h_t|, t < T, over this thread's points.
+  // GXC (16-row tiles, D == 1): the consumer is at the register limit, so the five running maxima
+  // live in the thread's LDS slots (Rg) instead of registers
+  float rq0 = 0.f, rq1 = 0.f, rq2 = 0.f, rq3 = 0.f, rh = 0.f;
+  if constexpr (GXC) {
+#pragma unroll
+    for (int k = 0; k < 5; ++k) Rg[k * 256 + ct] = 0.f;
+  }
   St4 nxt;
   load_tile(1, 0, nxt);
   load_x(2);                 // step 0: the producer computes tile (1, 0)
@@ -696,6 +717,27 @@ __global__ __launch_bounds__(SR_THREADS) void k_sweep_rows(Geom g, const bf16x8*
       } else {
         ti = tgt_quot(li, hp.rho[0], i1); tf = tgt_quot(lf, hp.rho[1], f1);
         tg = tgt_quot(lg, hp.rho[2], g1); to = tgt_quot(lo, hp.rho[3], o1);
+      }
+      if (a.range && rok) {
+        if constexpr (GXC) {   // one LDS slot at a time (the consumer is at the register limit)
+          auto upd = [&](int k, f32x4 a_, f32x4 t_) {
+            float m = Rg[k * 256 + ct];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) m = fmaxf(m, fabsf(a_[u] - t_[u]));
+            Rg[k * 256 + ct] = m;
+          };
+          upd(0, ai, ti); upd(1, af, tf); upd(2, ag, tg); upd(3, ao, to);
+          if (!last) upd(4, h1, f32x4{});
+        } else {
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            rq0 = fmaxf(rq0, fabsf(ai[u] - ti[u]));
+            rq1 = fmaxf(rq1, fabsf(af[u] - tf[u]));
+            rq2 = fmaxf(rq2, fabsf(ag[u] - tg[u]));
+            rq3 = fmaxf(rq3, fabsf(ao[u] - to[u]));
+            if (!last) rh = fmaxf(rh, fabsf(h1[u]));
+          }
+        }
       }
       if constexpr (GXP) {   // R = (phi(z) - tgt) phi'(z) into the z slot (0 past the last row)
         const float m = rok ? 1.f : 0.f;
@@ -769,6 +811,16 @@ __global__ __launch_bounds__(SR_THREADS) void k_sweep_rows(Geom g, const bf16x8*
       }
       SR_SYNC();             // end of step
     }
+  }
+  if (a.range) {
+    if constexpr (GXC) {
+      rq0 = Rg[ct]; rq1 = Rg[256 + ct]; rq2 = Rg[512 + ct]; rq3 = Rg[768 + ct]; rh = Rg[1024 + ct];
+    }
+    range_max(a.range + 0, rq0);
+    range_max(a.range + 1, rq1);
+    range_max(a.range + 2, rq2);
+    range_max(a.range + 3, rq3);
+    range_max(a.range + 4, rh);
   }
   if constexpr (GXC) {   // past the last step's barrier: its tile, then the slab (D == 1)
     const float* pp = &Px[((T - 1) * NT + NT - 1) & 1][0][cq][lane];
@@ -1080,9 +1132,11 @@ __global__ __launch_bounds__(kThreads) void k_atr_fused(Geom g, const float* x, 
 
 __global__ __launch_bounds__(kThreads) void k_reduce_g(int Kd, int H, int side, int p16, Hyper hp, const float* slab,
                                                          int nsplit, float* G, int* found, int* kpred,
-                                                         const DevStats* stats) {
+                                                         const DevStats* stats, float* range_reset) {
   const int64_t per_q = (int64_t)Kd * H;
   const int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+  // the h stage's k_atr3w has read the ranges: clear them for the sweep that follows (SweepT::range)
+  if (range_reset && i < 5) range_reset[i] = 0.f;
   if (i < 4) {
     found[i] = 0;   // this stage's line searches start undecided (no memset launch)
     if (kpred) kpred[i] = stats->k[2 * i];   // last step's x-side exponent (SpecX)
@@ -2860,7 +2914,24 @@ __global__ __launch_bounds__(kThreads) void k_check_lamh(Geom g, const float* __
   if (__any(nz) && (threadIdx.x & 63) == 0) atomicOr(flag, 1);
 }
 
+// range[5] = max over rows of sum_d |x[row][d]| (bounds |x dWx| for k_atr3w's fp16 scale)
+__global__ __launch_bounds__(kThreads) void k_x_l1max(int64_t rows, int D, const float* __restrict__ x,
+                                                        float* range) {
+  float m = 0.f;
+  for (int64_t r = (int64_t)blockIdx.x * kThreads + threadIdx.x; r < rows; r += (int64_t)gridDim.x * kThreads) {
+    float s = 0.f;
+    for (int d = 0; d < D; ++d) s += fabsf(x[r * D + d]);
+    m = fmaxf(m, s);
+  }
+  range_max(range + 5, m);
+}
+
 // ============================================================================ launchers
+
+void launch_x_l1max(const Geom& g, const float* x, float* range, hipStream_t s) {
+  const int nb = (int)std::max<int64_t>(1, std::min<int64_t>(cdiv64(g.BT(), kThreads), 1024));
+  k_x_l1max<<<nb, kThreads, 0, s>>>(g.BT(), g.D, x, range);
+}
 
 void launch_check_lamh(const Geom& g, const float* lh, int* flag, hipStream_t s) {
   const int64_t n = g.B * (int64_t)(g.T - 1) * (g.H / 4);
@@ -2999,11 +3070,11 @@ void launch_atr(const Geom& g, int side, const float* x, const float* Sh, const 
 }
 
 void launch_reduce_g(const Geom& g, int side, const Hyper& hp, const float* slab, int nsplit, float* G, int* found,
-                     int* kpred, const DevStats* stats, hipStream_t s, bool p16) {
+                     int* kpred, const DevStats* stats, hipStream_t s, bool p16, float* range_reset) {
   const int Kd = side == 0 ? g.D : g.H;
   const int64_t n = 4LL * Kd * g.H;
   k_reduce_g<<<cdiv64(n, kThreads), kThreads, 0, s>>>(Kd, g.H, side, p16 ? 1 : 0, hp, slab, nsplit, G, found, kpred,
-                                                       stats);
+                                                       stats, range_reset);
 }
 
 void launch_qgemm(const Geom& g, int side, const float* x, const float* Sh, const float* G, float* Q,
@@ -3033,6 +3104,42 @@ void launch_trial(const Geom& g, int pass, const float* zc, const float* tgt, co
 void launch_trial_debug(int64_t n, int tanh_gate, int kbase, const float* z, const float* tgt, const float* q,
                         double* part, int nblk, hipStream_t s) {
   k_trial_debug<<<nblk, kThreads, 0, s>>>(n, tanh_gate, kbase, z, tgt, q, part);
+}
+
+// Test hook (admm_debug_trace_resid): the residual R_q = (phi(z) - tgt) phi'(z) of one weight
+// stage, element by element with the activation of the kernel that formed it there (the
+// admm.py:302-312 residual), so a test can recompute G = rho A^T R on identical operands.
+//   mode 0: the persistent sweep's (sweep_point: sig_sweep2 / tanhf; the x stage's G_x partials)
+//   mode 1: k_resid_gx's (sig_pair / tanhf, the stored gates' activation)
+//   mode 2: phi_fast (the h stage's k_atr3w / k_atr_fused staging)
+template <int MODE>
+__global__ __launch_bounds__(kThreads) void k_debug_resid(int64_t n, const float* __restrict__ z,
+                                                           const float* __restrict__ tgt, float* __restrict__ R) {
+  for (int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x; i < 4 * n; i += (int64_t)gridDim.x * kThreads) {
+    const bool th = i / n == 2;
+    const float zz = z[i], tt = tgt[i];
+    float phi, dphi;
+    if (MODE == 2) {
+      if (th) phi_fast<true>(zz, phi, dphi);
+      else phi_fast<false>(zz, phi, dphi);
+    } else if (th) {
+      phi = tanhf(zz);
+      dphi = 1.f - phi * phi;
+    } else {
+      const SigPair sp = MODE == 0 ? sig_sweep2(zz) : sig_pair(zz);
+      phi = sp.s;
+      dphi = sp.s * sp.sc;
+    }
+    R[i] = (phi - tt) * dphi;
+  }
+}
+
+void launch_debug_resid(const Geom& g, int mode, const float* z, const float* tgt, float* R, hipStream_t s) {
+  const int64_t n = g.BT() * g.H;
+  const int nb = (int)std::min<int64_t>((4 * n + kThreads - 1) / kThreads, 8192);
+  if (mode == 0) k_debug_resid<0><<<nb, kThreads, 0, s>>>(n, z, tgt, R);
+  else if (mode == 1) k_debug_resid<1><<<nb, kThreads, 0, s>>>(n, z, tgt, R);
+  else k_debug_resid<2><<<nb, kThreads, 0, s>>>(n, z, tgt, R);
 }
 
 void launch_trial_reduce(const Geom& g, int pass, const double* part, int nblk, const int* found, double* sums,

@@ -106,6 +106,11 @@ struct SweepT {
   float* tgt;               // [4][B*T][H]: lam/rho + S of the updated state (k_sweep_rows; nullable)
   float* gx_slab;           // [blocks][4][D][H]: next x stage's X^T R partials (k_sweep_rows, D <= 16; nullable)
   const int* lamh_nz;       // k_sweep_rows: device flag, 0 = dual h is zero at every t < T (nullable: unknown)
+  // k_sweep_rows (nullable): running maxima, as float bits under atomicMax (zeroed beforehand), of
+  // the next step's weight-phase operands: [q] = max |phi(z) - tgt| of gate q (the x stage's
+  // residual before phi'), [4] = max |h_{t-1}| over t = 1..T (the h stage's H_prev).  They bound
+  // the h-side residual so k_atr3w can scale its fp16 operands (admm_split3.hip, kRange*)
+  float* range;
   int64_t r0, r1;           // sample rows [r0, r1) of this launch
 };
 void launch_sweep_t(const Geom& g, int t, const Weights& w, const Hyper& hp, const SweepT& a, hipStream_t s);
@@ -151,7 +156,7 @@ void launch_atr(const Geom& g, int side, const float* x, const float* Sh, const 
 void launch_reduce_g(const Geom& g, int side, const Hyper& hp, const float* Gslab, int nsplit, float* G, int* found,
                      int* kpred, const DevStats* stats,
                      hipStream_t s,
-                     bool p16 = true);
+                     bool p16 = true, float* range_reset = nullptr);   // range_reset: zero range[0..4] (SweepT::range)
 // Q[q][row][j] = sum_m A[row][m] * G[q][m][j]
 void launch_qgemm(const Geom& g, int side, const float* x, const float* Sh, const float* G, float* Q,
                   hipStream_t s);
@@ -163,6 +168,9 @@ void launch_trial(const Geom& g, int pass, const float* zc, const float* tgt, co
 // test hook: part[blk][J] for caller-provided z, tgt, q of one gate
 void launch_trial_debug(int64_t n, int tanh_gate, int kbase, const float* z, const float* tgt, const float* q,
                         double* part, int nblk, hipStream_t s);
+// test hook: R[4][BT][H] = (phi(z) - tgt) phi'(z) with the activation of the kernel that forms it
+// in the step (mode 0: the persistent sweep's, 1: k_resid_gx's, 2: phi_fast of the h stage)
+void launch_debug_resid(const Geom& g, int mode, const float* z, const float* tgt, float* R, hipStream_t s);
 // sums[q][0..J) = sum_blk part[q][k] ; sums[q][J] = sum d0^2 (= 2 f(W)/rho)
 void launch_trial_reduce(const Geom& g, int pass, const double* part, int nblk, const int* found, double* sums,
                          hipStream_t s);
@@ -214,8 +222,14 @@ int atr3_splits(const Geom& g);
 // two_waves (H == 256, atr3w_ok): k_atr3w, 8 waves with 128 accumulators (two per SIMD) instead of
 // k_atr3's 4 with 256; the same products in the same order, so bit-identical slabs
 bool atr3w_ok(const Geom& g);
+// range, dW non-null (H % 256 == 0, two_waves): the scaled-fp16 two-way split instead, with the
+// operand ranges the persistent sweep left (SweepT::range, plus [5] = max_row sum_d |x_d|) and the x
+// stage's decided update dW [4][D][H] (k_atr3w<2, true>)
 void launch_atr3(const Geom& g, const float* Sh, const float* zc, const float* tgt, float* slab, int nsplit,
-                 hipStream_t s, bool two_waves = true, int pieces = 3);
+                 hipStream_t s, bool two_waves = true, int pieces = 3, const float* range = nullptr,
+                 const float* dW = nullptr);
+// range[5] = max over rows of sum_d |x[row][d]| (atomicMax into a zeroed slot)
+void launch_x_l1max(const Geom& g, const float* x, float* range, hipStream_t s);
 // pieces = 3: f32-accurate split3 products; 2: two-way splits, three products (~2^-16 relative),
 // enough for the trial direction ("trial direction precision")
 // qpair (and qpair_ok: BT % 4 == 0): Q in the row-quad layout [q][row / 4][j][row % 4] that

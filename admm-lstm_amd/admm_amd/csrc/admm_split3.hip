@@ -480,10 +480,66 @@ struct Atr3wRing { float4 a[2], z[2], t[2]; };
 // products of mfma_split2 (~2^-16 relative per product, the accuracy of the reference's own fp32
 // sums over B*T rows; DESIGN.md "h-side gradient on two-way splits"), half the matrix work and
 // two thirds of the staging
-template <bool TANH, int NP>
+// F16 (NP = 2): the two pieces are fp16 instead of bf16 (hi = rn(a), lo = rn(a - hi): 22 bits,
+// ~2^-22 relative per piece pair, 2^-20.4 per product at worst -- f32-accurate once summed with the
+// f32 accumulation of thousands of rows), on the same matrix rate (v_mfma_f32_32x32x16_f16).  fp16
+// has 5 exponent bits, so both operands are first scaled by exact powers of two that put their
+// largest possible magnitude at 2^14 (< 65504): sH from max |H_prev| and sR from a bound on |R|
+// (atr_scales), undone on the slab (exact).  Values 2^17 below the bound lose relative precision in
+// the lo piece (fp16 subnormals), i.e. absolute errors below 2^-39 of the bound.
+typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+__device__ __forceinline__ void split2h(f32x4 a, bf16x4& p0, bf16x4& p1) {
+  const f16x4 h0 = __builtin_convertvector(a, f16x4);
+  const f16x4 h1 = __builtin_convertvector(a - __builtin_convertvector(h0, f32x4), f16x4);
+  p0 = __builtin_bit_cast(bf16x4, h0);
+  p1 = __builtin_bit_cast(bf16x4, h1);
+}
+// the three products of fp16 two-way splits (pieces carried as 16-bit patterns in bf16 vectors)
+__device__ __forceinline__ f32x16 mfma_split2h(const bf16x8 (&a)[3], const bf16x8 (&b)[3], f32x16 acc) {
+  const f16x8 a0 = __builtin_bit_cast(f16x8, a[0]), a1 = __builtin_bit_cast(f16x8, a[1]);
+  const f16x8 b0 = __builtin_bit_cast(f16x8, b[0]), b1 = __builtin_bit_cast(f16x8, b[1]);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1, b0, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0, b1, acc, 0, 0, 0);
+  acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(a0, b0, acc, 0, 0, 0);
+  return acc;
+}
+
+// The scales of gate q's fp16 operands, from the ranges the last persistent sweep left (range[q] =
+// max |phi(z) - tgt| over the x stage's z, range[4] = max |H_prev|, range[5] = max_row sum_d |x_d|)
+// and the x stage's decided update dWx (the h stage's z is z + x dWx): |R| = |phi(z') - tgt| phi'(z')
+// <= max|phi(z) - tgt| + |x dWx| (phi 1-Lipschitz, phi' <= 1).  The bound carries a factor 2 and an
+// absolute 2^-16 for the rounding of z' and the ulps between the kernels' activation codes.
+// Computed identically by every workgroup (512 threads); returns {sH, sR}.
+__device__ __forceinline__ float2 atr_scales(const Geom& g, int q, const float* __restrict__ range,
+                                             const float* __restrict__ dW, float* red /* LDS, >= 8 */) {
+  const int n = g.D * g.H;
+  const float* dq = dW + (int64_t)q * n;
+  float m = 0.f;
+  for (int i = threadIdx.x; i < n; i += A3W_THREADS) m = fmaxf(m, fabsf(dq[i]));
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+  __syncthreads();
+  float dwm = 0.f;
+#pragma unroll
+  for (int w = 0; w < A3W_THREADS / 64; ++w) dwm = fmaxf(dwm, red[w]);
+  __syncthreads();   // red is reused
+  const float rb = 2.f * (range[q] + range[5] * dwm + 0x1p-16f);
+  const float hb = 2.f * range[4] + 0x1p-30f;
+  auto scale = [](float b) {   // 2^(13 - floor(log2 b)): b * scale <= 2^14
+    const int e = 13 - ilogbf(b);
+    return ldexpf(1.f, e < -60 ? -60 : e > 60 ? 60 : e);
+  };
+  return make_float2(scale(hb), scale(rb));
+}
+
+template <bool TANH, int NP, bool F16 = false>
 __device__ __forceinline__ void atr3w_body(const Geom& g, int q, int sp, int nsplit, int mb, int nb,
                                            const float* __restrict__ Sh, const float* __restrict__ zq,
-                                           const float* __restrict__ tq, float* __restrict__ slab, __bf16* img) {
+                                           const float* __restrict__ tq, float* __restrict__ slab, __bf16* img,
+                                           float2 scl = make_float2(1.f, 1.f)) {
+  static_assert(!F16 || NP == 2, "fp16 operands come in two pieces");
   using P = A3<256>;
   const int H = g.H;
   const int64_t BT = g.BT();
@@ -517,14 +573,16 @@ __device__ __forceinline__ void atr3w_body(const Geom& g, int q, int sp, int nsp
     __bf16* B = A + NP * P::PA;
     bf16x4 p0, p1, p2;
     auto pieces = [&](f32x4 v) {
-      if constexpr (NP == 3) split3(v, p0, p1, p2);
+      if constexpr (F16) split2h(v, p0, p1);
+      else if constexpr (NP == 3) split3(v, p0, p1, p2);
       else split2(v, p0, p1);
     };
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const int rr = 2 * rg + i;
       const int o = a3_off(rr, 4 * lane);
-      pieces(f32x4{R.a[i].x, R.a[i].y, R.a[i].z, R.a[i].w});
+      if constexpr (F16) pieces(f32x4{R.a[i].x, R.a[i].y, R.a[i].z, R.a[i].w} * scl.x);
+      else pieces(f32x4{R.a[i].x, R.a[i].y, R.a[i].z, R.a[i].w});
       *reinterpret_cast<bf16x4*>(A + o) = p0;
       *reinterpret_cast<bf16x4*>(A + P::PA + o) = p1;
       if constexpr (NP == 3) *reinterpret_cast<bf16x4*>(A + 2 * P::PA + o) = p2;
@@ -538,7 +596,8 @@ __device__ __forceinline__ void atr3w_body(const Geom& g, int q, int sp, int nsp
         phi_fast<TANH>(zz[u], phi, dphi);
         rv[u] = ok ? (phi - tt[u]) * dphi : 0.f;
       }
-      pieces(rv);
+      if constexpr (F16) pieces(rv * scl.y);
+      else pieces(rv);
       *reinterpret_cast<bf16x4*>(B + o) = p0;
       *reinterpret_cast<bf16x4*>(B + P::PR + o) = p1;
       if constexpr (NP == 3) *reinterpret_cast<bf16x4*>(B + 2 * P::PR + o) = p2;
@@ -573,6 +632,7 @@ __device__ __forceinline__ void atr3w_body(const Geom& g, int q, int sp, int nsp
 #pragma unroll
       for (int ni = 0; ni < 2; ++ni) {
         if (A3W_ABL & 2) acc[mi][ni][0] += (float)a[0][0] * (float)b[ni][0][0];   // ablation: no MFMAs
+        else if constexpr (F16) acc[mi][ni] = mfma_split2h(a, b[ni], acc[mi][ni]);
         else if constexpr (NP == 3) acc[mi][ni] = mfma_split3(a, b[ni], acc[mi][ni]);
         else acc[mi][ni] = mfma_split2(a, b[ni], acc[mi][ni]);
       }
@@ -599,28 +659,32 @@ __device__ __forceinline__ void atr3w_body(const Geom& g, int q, int sp, int nsp
     }
   }
   float* out = slab + ((int64_t)sp * 4 + q) * H * H + (int64_t)(256 * mb) * H + 256 * nb + wc * 64 + (lane & 31);
+  const float inv = F16 ? 1.f / (scl.x * scl.y) : 1.f;   // a power of two: exact
 #pragma unroll
   for (int mi = 0; mi < 4; ++mi)
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int m = wr * 128 + mi * 32 + acc_row(r, lane);
 #pragma unroll
-      for (int ni = 0; ni < 2; ++ni) out[(int64_t)m * H + ni * 32] = acc[mi][ni][r];
+      for (int ni = 0; ni < 2; ++ni) out[(int64_t)m * H + ni * 32] = F16 ? acc[mi][ni][r] * inv : acc[mi][ni][r];
     }
 }
 
-template <int NP>
+template <int NP, bool F16 = false>
 __global__ __launch_bounds__(A3W_THREADS, 1) void k_atr3w(Geom g, const float* __restrict__ Sh,
                                                          const float* __restrict__ zc, const float* __restrict__ tgt,
-                                                         float* __restrict__ slab, int nsplit) {
+                                                         float* __restrict__ slab, int nsplit,
+                                                         const float* __restrict__ range, const float* __restrict__ dW) {
   __shared__ __attribute__((aligned(16))) __bf16 img[2 * NP * (A3<256>::PA + A3<256>::PR)];
   int lid = xcd_swizzle(blockIdx.x, gridDim.x);
   const int q = lid % 4;          // the 4 gates of one split share the Hprev rows: same XCD
   lid /= 4;
   const int nt = g.H / 256, tl = lid % (nt * nt), sp = lid / (nt * nt);
   const int64_t n = g.BT() * g.H;
-  if (q == 2) atr3w_body<true, NP>(g, q, sp, nsplit, tl / nt, tl % nt, Sh, zc + q * n, tgt + q * n, slab, img);
-  else atr3w_body<false, NP>(g, q, sp, nsplit, tl / nt, tl % nt, Sh, zc + q * n, tgt + q * n, slab, img);
+  float2 scl = make_float2(1.f, 1.f);
+  if constexpr (F16) scl = atr_scales(g, q, range, dW, reinterpret_cast<float*>(img));
+  if (q == 2) atr3w_body<true, NP, F16>(g, q, sp, nsplit, tl / nt, tl % nt, Sh, zc + q * n, tgt + q * n, slab, img, scl);
+  else atr3w_body<false, NP, F16>(g, q, sp, nsplit, tl / nt, tl % nt, Sh, zc + q * n, tgt + q * n, slab, img, scl);
 }
 
 }  // namespace
@@ -642,12 +706,14 @@ int atr3_splits(const Geom& g) {
 bool atr3w_ok(const Geom& g) { return g.H % 256 == 0; }
 
 void launch_atr3(const Geom& g, const float* Sh, const float* zc, const float* tgt, float* slab, int nsplit,
-                 hipStream_t s, bool two_waves, int pieces) {
+                 hipStream_t s, bool two_waves, int pieces, const float* range, const float* dW) {
   dim3 grid((g.H / A3_BM) * (g.H / A3_BN) * 4 * nsplit);
   if (two_waves && atr3w_ok(g)) {   // 256 x 256 blocks of each gate's G, nsplit row ranges
-    const int nt = g.H / 256;
-    if (pieces == 2) k_atr3w<2><<<4 * nt * nt * nsplit, A3W_THREADS, 0, s>>>(g, Sh, zc, tgt, slab, nsplit);
-    else k_atr3w<3><<<4 * nt * nt * nsplit, A3W_THREADS, 0, s>>>(g, Sh, zc, tgt, slab, nsplit);
+    const int nt = g.H / 256, nb = 4 * nt * nt * nsplit;
+    if (range && dW)   // scaled fp16 two-way splits (f32-accurate, the cost of pieces == 2)
+      k_atr3w<2, true><<<nb, A3W_THREADS, 0, s>>>(g, Sh, zc, tgt, slab, nsplit, range, dW);
+    else if (pieces == 2) k_atr3w<2><<<nb, A3W_THREADS, 0, s>>>(g, Sh, zc, tgt, slab, nsplit, nullptr, nullptr);
+    else k_atr3w<3><<<nb, A3W_THREADS, 0, s>>>(g, Sh, zc, tgt, slab, nsplit, nullptr, nullptr);
   } else {
     k_atr3<<<grid, kThreads, 0, s>>>(g, Sh, zc, tgt, slab, nsplit);
   }

@@ -197,6 +197,14 @@ int admm_debug_workspace(AdmmCtx* ctx, int32_t which, void* dst, int64_t bytes, 
    library's own search direction. */
 int admm_debug_trace(AdmmCtx* ctx, float* gx, float* gh);
 
+/* Test hook: while set, every admm_step also writes the residual each weight stage formed its
+   gradient from, R_q = (phi(z) - dual/rho - gate) phi'(z) (admm.py:302-312), element by element as
+   the stage's gradient kernel formed it (same activation code), into the caller's device buffers
+   rx (x stage) and rh (h stage), each [4][B*T][H] with row b*T + (t-1).  With admm_debug_trace's
+   G, a test recomputes G = rho A^T R on the identical operands (A = X or H_prev) in fp64 and
+   measures the gradient GEMM's own arithmetic error.  NULL pointers turn the copy off. */
+int admm_debug_trace_resid(AdmmCtx* ctx, float* rx, float* rh);
+
 /* Test hook: replay given line-search decisions.  While set (k8 != NULL), every admm_step still
    runs each search but then applies k8[2 q + side] (q = i,f,g,o; side 0 = x2q, 1 = h2q) as the
    exponent of admm.py:331-343 and, for the h_T search (admm.py:474-482), theta = 0.1 doubled

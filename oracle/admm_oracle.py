@@ -452,7 +452,7 @@ def fp64_decisions(x, y, W, S, L, hyper: Hyper, global_batch: Optional[int] = No
             'grads': [r['grad'] for r in rec['weights']]}
 
 
-def fp64_search(q: str, z, tgt, A, G, rho: float, T: int, kmax: int = 64):
+def fp64_search(q: str, z, tgt, A, G, rho: float, T: int, kmax: int = 64, orig: bool = False):
     """The backtracking search of ``admm.py:316-343`` for ONE gate weight, in fp64, from given
     inputs: z [R, H] the pre-activations at W, tgt [R, H] = dual/rho + gate, A [R, K] the rows
     of the side's input (X or H_prev), G [K, H] the (rho-scaled) gradient, i.e. the search
@@ -467,7 +467,13 @@ def fp64_search(q: str, z, tgt, A, G, rho: float, T: int, kmax: int = 64):
     deciding comparisons (the last failing one and the passing one); eps_g = |G - rho A^T R| / |G|
     with R = (phi(z) - tgt) phi'(z) in fp64 from the same z and tgt: how much of G itself is the
     fp32 rounding of the residual (phi(z) - tgt is a difference of O(1) numbers that agree to
-    ~1e-7 when the ADMM residuals are that small) -- recorded, it is the same in the reference."""
+    ~1e-7 when the ADMM residuals are that small) -- recorded, it is the same in the reference.
+
+    orig=True also evaluates the reference's test in its ORIGINAL form with the same G,
+    f(W + s G) - f(W) > (1 + T/2) |G|^2 s, f in fp64 from the same z and tgt
+    (f(W + s G) - f(W) = 0.5 rho sum[D^2 + 2 d0 D]), and returns (k, margin, eps_g, k_orig,
+    margin_orig).  The two forms differ by s (<grad f, G> - |G|^2): zero when G is the exact
+    gradient of the fp64 objective, of relative size ~eps_g (2/T) against the threshold otherwise."""
     act = torch.tanh if q == 'g' else torch.sigmoid
     z, tgt, A, G = (v.to(torch.float64) for v in (z, tgt, A, G))
     p0 = act(z)
@@ -491,4 +497,17 @@ def fp64_search(q: str, z, tgt, A, G, rho: float, T: int, kmax: int = 64):
         if not rem > est:
             break
     ms = [abs(a - b) / b for a, b in tests[-2:] if b > 0]
-    return len(tests) - 1, (min(ms) if ms else float('inf')), eps_g
+    out = (len(tests) - 1, (min(ms) if ms else float('inf')), eps_g)
+    if not orig:
+        return out
+    c1 = (1.0 + 0.5 * T) * float((G * G).sum())
+    tests = []
+    for k in range(kmax):
+        s = 2.0 ** -k
+        D = act(z + qd * s) - p0
+        inc = 0.5 * rho * float((D * D + 2.0 * d0 * D).sum())
+        tests.append((inc, c1 * s))
+        if not inc > c1 * s:
+            break
+    ms = [abs(a - b) / b for a, b in tests[-2:] if b > 0]
+    return out + (len(tests) - 1, (min(ms) if ms else float('inf')))

@@ -62,6 +62,11 @@ CASES = {
     'c5_1gpu':      ('no_dual_y', False, 'rw', 4096, 64, 1, 512, 3, False, 'GoogleStock'),
     # C4's global problem (65536 samples; the 8-GPU run shards exactly this) on one device
     'c4g':          ('admm', False, 'uniform', 65536, 32, 16, 256, 3, False, 'GoogleStock'),
+    # perturbed starting state (golden_io.perturb_state: 1e-2 noise on gates and duals), so that the
+    # eight weight updates move the weights far above fp32 resolution at H >= 256 (the sizes where
+    # the library runs its split-bf16 h-stage GEMMs and row-pair trials); full weights every step
+    't4_pert_h256': ('admm', False, 'uniform', 1024, 8, 16, 256, 3, False, 'GoogleStock'),
+    't4_pert_h512': ('no_dual_y', False, 'rw', 512, 8, 1, 512, 3, False, 'GoogleStock'),
 }
 
 # compact cases: which steps keep their full weights (the others keep x2q/out in full and
@@ -70,7 +75,11 @@ CASES = {
 # fp32 line-search decisions compare with fp64 ones from the same state
 COMPACT = {'c3': {'full_w': (1, 2, 3, 4, 5), 'fp64': True},
            'c5_1gpu': {'full_w': (3,), 'fp64': False},
-           'c4g': {'full_w': (3,), 'fp64': False}}
+           'c4g': {'full_w': (3,), 'fp64': False},
+           't4_pert_h256': {'full_w': (1, 2, 3), 'fp64': True},
+           't4_pert_h512': {'full_w': (1, 2, 3), 'fp64': True}}
+# perturbed cases: golden_io.perturb_state(seed, scale) right after the optimizer is constructed
+PERTURB = {'t4_pert_h256': {'seed': 11, 'scale': 1e-2}, 't4_pert_h512': {'seed': 11, 'scale': 1e-2}}
 WSTRIDE = 16
 
 
@@ -194,6 +203,12 @@ def run_case(name):
             return float(loss_fn(model(vx), vy)) if vx is not None else None
 
     opt = mod.ADMMBasedOptimizer(model, (x, y), pdict, verbose=False)
+    pert = PERTURB.get(name)
+    if pert:
+        sys.path.insert(0, os.path.dirname(OUT))
+        from golden_io import perturb_state
+        sys.path.pop(0)
+        perturb_state(opt.gates, opt.duals, B, T, H, pert['seed'], pert['scale'])
 
     def snap_state(prefix):
         for q in GATES:
@@ -256,6 +271,8 @@ def run_case(name):
                            'y_sha256': hashlib.sha256(y.numpy().tobytes()).hexdigest(),
                            'inputs': f'make_inputs({gen!r}, {B}, {T}, {D}) (SURVEY.md 8(d) generator)'}
         meta['fp64'] = fp64_recs
+    if pert:
+        meta['perturb'] = pert
     arrays['meta_json'] = np.array(json.dumps(meta))
     path = os.path.join(OUT, f'{name}.npz')
     np.savez_compressed(path, **arrays)

@@ -76,6 +76,24 @@ class Golden:
         return [len(v) - 1 for v in self.searches[step - 1]['weights']]
 
 
+def perturb_state(gates, duals, B: int, T: int, H: int, seed: int = 11, scale: float = 1e-2):
+    """The perturbed starting state of the ``t4_pert_*`` fixtures (and of the GPU line-search
+    test ``test_line_search_matches_fp64_oracle``): seeded ``scale``-sized noise on every gate at
+    t >= 1 and on the i, f, g, o, c duals, so that the weight gradients are far above the fp32
+    rounding of the residual and the eight weight updates move the weights visibly
+    (``admm.py:282-343``).  The dual of h stays zero (the reference ascends it only at T).
+    ``gates`` / ``duals`` are the optimizer's dicts of [B, T+1, H] tensors, edited in place."""
+    gen = torch.Generator().manual_seed(seed)
+    with torch.no_grad():
+        for q in GATES6:
+            noise = scale * torch.randn(B, T + 1, H, generator=gen)
+            noise[:, 0] = 0
+            gates[q].add_(noise.to(gates[q].device))
+            if q != 'h':
+                duals[q].copy_(scale * torch.randn(B, T + 1, H, generator=gen))
+    return gates, duals
+
+
 def make_inputs(gen: str, B: int, T: int, D: int):
     """SURVEY.md 8(d) synthetic inputs (the generators tests/golden/make_golden.py ran the
     reference on): uniform (seed 1234) and random-walk windows (seed 7)."""
@@ -95,6 +113,9 @@ def make_inputs(gen: str, B: int, T: int, D: int):
 # step fixtures (goog_cols45.npz holds the C1 input columns, not a step trajectory); the compact
 # full-size ones are run by their own tests
 _NAMES = sorted(f[:-4] for f in os.listdir(GOLDEN) if f.endswith('.npz') and not f.startswith('goog_'))
-COMPACT = [n for n in _NAMES if Golden(n).compact]
-ALL = [n for n in _NAMES if n not in COMPACT]
+# perturbed-state fixtures start from perturb_state(), not from the optimizer's own initial state:
+# tests/test_gpu_weight_phase.py runs them
+PERTURBED = [n for n in _NAMES if Golden(n).meta.get('perturb')]
+COMPACT = [n for n in _NAMES if Golden(n).compact and n not in PERTURBED]
+ALL = [n for n in _NAMES if n not in COMPACT and n not in PERTURBED]
 FULL = [n for n in ALL if Golden(n).full_state]

@@ -96,6 +96,7 @@ static void check_args() {
   CHECK(admm_comm_unique_id(nullptr, 1024) == ADMM_EINVAL);
   CHECK(admm_debug_trace(nullptr, nullptr, nullptr) != ADMM_OK);
   CHECK(admm_debug_force(nullptr, nullptr, 0) != ADMM_OK);
+  CHECK(admm_debug_trace_resid(nullptr, nullptr, nullptr) != ADMM_OK);
   CHECK(admm_debug_own(nullptr, nullptr, nullptr) != ADMM_OK);
   CHECK(admm_debug_workspace(nullptr, 0, nullptr, 0, nullptr) < 0);
   const float* w4[4] = {nullptr, nullptr, nullptr, nullptr};
@@ -179,6 +180,8 @@ static void run_context(int64_t B, int T, int D, int H, int O, int variant, int 
   // the debug hooks with caller buffers, then off again
   float *gx = zeros((size_t)4 * D * H), *gh = zeros((size_t)4 * H * H);
   CHECK(admm_debug_trace(ctx, gx, gh) == ADMM_OK);
+  float *rx = zeros((size_t)4 * B * T * H), *rh = zeros((size_t)4 * B * T * H);
+  CHECK(admm_debug_trace_resid(ctx, rx, rh) == ADMM_OK);
   auto finite_dev = [&](const float* dptr, size_t n) {
     std::vector<float> h(n);
     if (hipMemcpy(h.data(), dptr, n * 4, hipMemcpyDeviceToHost) != hipSuccess) return false;
@@ -208,6 +211,7 @@ static void run_context(int64_t B, int T, int D, int H, int O, int variant, int 
     if (s == 2) CHECK(admm_invalidate_cache(ctx) == ADMM_OK);   // next step rebuilds the caches
   }
   CHECK(admm_debug_trace(ctx, nullptr, nullptr) == ADMM_OK);
+  CHECK(admm_debug_trace_resid(ctx, nullptr, nullptr) == ADMM_OK);
   // replay: force the exponents the last step took (forcing arbitrary small ones can overflow
   // the weights), and one doubling more for the h_T search
   AdmmStats prev{};
@@ -242,7 +246,7 @@ static void run_context(int64_t B, int T, int D, int H, int O, int variant, int 
   CHECK(hipDeviceSynchronize() == hipSuccess);
   CHECK(finite_dev(oa, (size_t)B * O));
   CHECK(admm_destroy(ctx) == ADMM_OK);
-  for (float* q : {gx, gh, zc, hs, cs, oa}) (void)hipFree(q);
+  for (float* q : {gx, gh, rx, rh, zc, hs, cs, oa}) (void)hipFree(q);
   for (float* q : owned) (void)hipFree(q);
 }
 

@@ -72,10 +72,10 @@ def _same_input_fp64(g, opt, pre, gx, gh, model, dev):
     for qi, q in enumerate('ifgo'):
         rho = float(opt.rhos[q])
         tgt = (L[q][:, 1:, :] / opt.rhos[q].to(dev) + S[q][:, 1:, :]).reshape(B * T, H)   # admm.py:308-309, fp32
-        out.append(O.fp64_search(q, zc[qi], tgt, X, gx[qi], rho, T))
+        out.append(O.fp64_search(q, zc[qi], tgt, X, gx[qi], rho, T, orig=True))
         dwx = getattr(model, f'x2{q}').detach().double() - W0[f'x2{q}'].double()
         zh = (zc[qi].double() + X.double() @ dwx).float()   # the h stage's z, fp32 as the library holds it
-        out.append(O.fp64_search(q, zh, tgt, Hp, gh[qi], rho, T))
+        out.append(O.fp64_search(q, zh, tgt, Hp, gh[qi], rho, T, orig=True))
         del tgt, zh
     return out
 
@@ -145,7 +145,7 @@ def _write(name, recs, g):
             d['fp64_at_ref_state'] = g.fp64_ks(r['step'])
         summ.append(d)
     with open(os.path.join(out, f'parity_{name}.json'), 'w') as f:
-        json.dump(summ, f, indent=1)
+        json.dump({'steps': summ, 'orig_form': orig_form_departures(recs)}, f, indent=1)
 
 
 @pytest.mark.parametrize('name', COMPACT)
@@ -167,7 +167,8 @@ def test_fullsize_matches_reference(name, dev, monkeypatch):
             # fp32 rounding of the stored state moves by g_rel_diff relative, which moves the
             # decision boundary (a Rayleigh quotient along G) by about as much
             k64, margin = r['fp64'][i]
-            tie = max(1e-3, 2.0 * r['g_rel_diff'][i])
+            # (capped at 1e-2 whatever g_rel_diff is: a wider band would let one doubling pass anywhere)
+            tie = max(1e-3, min(1e-2, 2.0 * r['g_rel_diff'][i]))
             assert a == k64 or (margin < tie and abs(a - k64) <= 1), (s, i, r['k'], r['ref_k'], r['fp64'],
                                                                         r['g_rel_diff'])
     _check_follows_fp64(recs)
@@ -192,7 +193,8 @@ def _check_follows_fp64(recs):
     as here.  Nearly every search must be a checked one."""
     checked = 0
     for r in recs:
-        for i, (a, (k64, margin, _eps)) in enumerate(zip(r['k'], r['same_input_fp64'])):
+        for i, (a, si) in enumerate(zip(r['k'], r['same_input_fp64'])):
+            k64, margin = si[:2]
             if margin > 0.01:
                 checked += 1
                 assert a == k64, (r['step'], i, r['k'], r['same_input_fp64'])
@@ -200,6 +202,23 @@ def _check_follows_fp64(recs):
                 assert abs(a - k64) <= 1, (r['step'], i, r['k'], r['same_input_fp64'])
     assert checked >= 6 * len(recs), (checked, [r['same_input_fp64'] for r in recs])
     return checked
+
+
+def orig_form_departures(recs):
+    """Searches where the library's exponent differs from the fp64 search in the reference's
+    ORIGINAL form (f(W + sG) - f(W) against (1 + T/2)|G|^2 s, same G, z and tgt) by more than the
+    margin of that decision -- the cost of deciding on the remainder past the first-order term
+    (DESIGN.md section 2).  Recorded per case (summary['orig_form'])."""
+    n, dep = 0, []
+    for r in recs:
+        for i, (a, si) in enumerate(zip(r['k'], r['same_input_fp64'])):
+            if len(si) < 5:
+                continue
+            n += 1
+            if a != si[3] and si[4] > 0.01:
+                dep.append({'step': r['step'], 'search': i, 'k': a, 'k_orig': si[3], 'margin_orig': si[4],
+                            'eps_g': si[2]})
+    return {'searches': n, 'departures': dep}
 
 
 def test_line_search_follows_fp64_c2(dev):
@@ -259,14 +278,14 @@ def test_c1_forced_replay_all_epochs(dev):
                      'ref_k': ref_k, 'own_k': own, 'theta_h_own': th_own.value})
         assert tr == pytest.approx(g.losses[s], rel=LOSS_RTOL), (s, tr, g.losses[s])
         assert va == pytest.approx(g.val_losses[s], rel=LOSS_RTOL), (s, va, g.val_losses[s])
+        same = _same_input_fp64(g, opt, (zc, W0, S, L), gx, gh, model, dev)
+        recs[-1]['same_input_fp64'] = same
         if own != ref_k:
             departures += 1
-            same = _same_input_fp64(g, opt, (zc, W0, S, L), gx, gh, model, dev)
-            recs[-1]['same_input_fp64'] = same
             for i, (a, r) in enumerate(zip(own, ref_k)):
                 if a == r:
                     continue
-                k64, margin, _eps = same[i]
+                k64, margin = same[i][:2]
                 if a < 0:      # the library's first window did not decide: fp64 must be beyond it too
                     assert k64 >= 16, (s, i, own, ref_k, same)
                 elif margin > 0.01:
@@ -277,5 +296,8 @@ def test_c1_forced_replay_all_epochs(dev):
     out = os.environ.get('ADMM_PARITY_OUT')
     if out:
         os.makedirs(out, exist_ok=True)
+        # the remainder rule against the reference's original form at T = 10 (own decisions)
+        orig = orig_form_departures([{'step': r['epoch'], 'k': r['own_k'], 'same_input_fp64': r['same_input_fp64']}
+                                     for r in recs])
         with open(os.path.join(out, 'parity_c1_forced.json'), 'w') as f:
-            json.dump({'departures': departures, 'epochs': recs}, f, indent=1)
+            json.dump({'departures': departures, 'orig_form': orig, 'epochs': recs}, f, indent=1)

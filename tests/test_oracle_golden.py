@@ -8,7 +8,7 @@ operands, and the full primal/dual state.
 import pytest
 import torch
 
-from golden_io import ALL, FULL, GATES6, WEIGHT_NAMES, Golden
+from golden_io import ALL, FULL, GATES6, PERTURBED, WEIGHT_NAMES, Golden, perturb_state
 from oracle import admm_oracle as O
 
 FAST = [n for n in ALL if not n.startswith('t1_')] + ['t1_gstock']
@@ -63,6 +63,27 @@ def test_trajectory_bit_exact(name):
                 assert torch.equal(st.L[q], L[q]), (s, q)
             assert torch.equal(st.S['a'], S['a'])
             assert torch.equal(st.L['y'], L['y'])
+
+
+@pytest.mark.parametrize('name', PERTURBED)
+def test_perturbed_trajectory_bit_exact(name):
+    """The t4_pert_* fixtures: the reference stepped from a perturbed state (golden_io.perturb_state)
+    at H = 256 and H = 512, the sizes of the library's fast weight-stage kernels.  The oracle from the
+    same perturbed state reproduces every weight, search comparison and loss bit for bit."""
+    g = Golden(name)
+    torch.manual_seed(0)
+    W = O.init_weights(g.D, g.H, g.O)
+    st = O.init_state(g.x, g.y, W)
+    perturb_state(st.S, st.L, g.B, g.T, g.H, g.perturb['seed'], g.perturb['scale'])
+    stp = O.Stepper(O.Hyper.from_dict(g.params, g.variant, g.with_dual_y))
+    for s in range(1, g.steps + 1):
+        rec = stp.step(st)
+        assert [r['k'] for r in rec['weights']] == g.ks(s), f'step {s}'
+        for r, ref in zip(rec['weights'], g.searches[s - 1]['weights']):
+            assert [(a, b, w) for a, b, w in r['tests']] == [tuple(v) for v in ref]
+        for k in WEIGHT_NAMES:
+            assert torch.equal(st.W[k], g.t(f'w{s}_{k}')), (s, k)
+        assert O.mse(g.x, g.y, st.W) == g.losses[s]
 
 
 @pytest.mark.parametrize('name', FULL)

@@ -115,21 +115,12 @@ struct AdmmCtx {
   int nblk_resid = 1, nblk_trial = 1, nblk_rx = 1;
   int* found = nullptr;
   int* pick = nullptr;
-  int sweep_split = 2;     // sample parts of the sweep, one stream each (ADMM_SWEEP_SPLIT)
+  int sweep_split = 2;     // sample parts of the per-t sweep, one stream each
   bool sweep_rows = false; // whole sweep as one persistent launch (k_sweep_rows; ADMM_SWEEP_ROWS=0 disables)
   float* swt = nullptr;    // its B-operand image of the weights
   bool split3 = false;     // h-stage GEMMs on split bf16 MFMAs (admm_split3.hip; ADMM_SPLIT3=0 disables)
-  // pieces of the trial direction GEMM Q = Hprev G: 1 = Hprev in two bf16 pieces, G in one (G
-  // rounded to bf16, ~2^-9 relative per element: the line-search remainder moves by ~0.4 %, against
-  // decision margins of >= 12 % on the h side at C3 and C5); 2 = two-piece G (~2^-16); 3 = split3,
-  // f32-accurate (ADMM_Q_PIECES).  Q only enters the line-search increments (DESIGN.md "trial
-  // direction precision"); G itself, which updates the weights, is not rounded.
-  int q_pieces = 1;
-  // split pieces of the h-side gradient G_h = rho Hprev^T R (k_atr3w): 3 = split3's six products,
-  // f32-accurate (tests/test_gpu_weight_phase.py: within the error of an fp32 GEMM of the same
-  // operands); ADMM_ATR_PIECES=2: two-way bf16 splits, ~2^-16 relative per product, which measured
-  // 1.3-3.7x a torch fp32 GEMM's error on perturbed states -- not f32-equivalent
-  int atr_pieces = 3;
+  // the h-side gradient G_h = rho Hprev^T R (k_atr3w) on split3's six products, f32-accurate
+  // (tests/test_gpu_weight_phase.py: within the error of an fp32 GEMM of the same operands) ...
   // ... unless the operand ranges are known: the h-side gradient then runs on scaled fp16 two-way
   // splits (k_atr3w<2, true>: f32-accurate at the matrix work of two pieces; ADMM_ATR_F16=0: off).
   // range [8] (device): SweepT::range's maxima from the last persistent sweep ([0..4], valid when
@@ -140,12 +131,6 @@ struct AdmmCtx {
   // pass 0 of a gate whose last exponent was past the first window also sums the per-candidate
   // elements' polynomial, so the exponents past it are decided without pass 1 (ADMM_P16=0: off)
   bool p16 = true;
-  bool atr3w = true;       // k_atr3w (two waves per SIMD) for the h-side gradient; ADMM_ATR3W=0: k_atr3
-  // Q in the row-quad layout (k_qgemm3 -> k_trial_rows<1>): 2 = bf16 elements (default), 1 = f32,
-  // 0 = row-major f32 (ADMM_QPAIR)
-  int qpair = 2;
-  // Q = Hprev G with the G image resident in LDS (k_qgemm_res; ADMM_QRES=0: k_qgemm3)
-  bool qres = true;
   float* gimg = nullptr;   // split image of G_h for k_qgemm3
   hipStream_t sx[kMaxSweepStreams - 1] = {};
   hipEvent_t ev_fork = nullptr, ev_join[kMaxSweepStreams - 1] = {};
@@ -308,15 +293,15 @@ int stage_weights(AdmmCtx* c, int side, hipStream_t s) {
   } else if (fast && c->split3) {
     ns = atr3_splits(g);
     // scaled fp16 operands once a persistent sweep has left the operand ranges of this state
-    const bool f16 = c->atr_f16 && c->range_valid && c->atr3w && atr3w_ok(g);
+    const bool f16 = c->atr_f16 && c->range_valid;
     if (f16 && !c->x1_valid) {
       HIP_TRY(hipMemsetAsync(c->range + 5, 0, sizeof(float), s));
       launch_x_l1max(g, c->buf.x, c->range, s);
       c->x1_valid = true;
     }
     ProfScope ps(c, ADMM_PROF_ATR_H, s);
-    launch_atr3(g, c->buf.gates[ADMM_H], zh, c->tgt, c->gslab, ns, s, c->atr3w, c->atr_pieces,
-                f16 ? c->range : nullptr, f16 ? c->dW : nullptr);
+    launch_atr3(g, c->buf.gates[ADMM_H], zh, c->tgt, c->gslab, ns, s, f16 ? c->range : nullptr,
+                f16 ? c->dW : nullptr);
   } else if (fast) {
     ns = atr_splits(g, 1);
     ProfScope ps(c, ADMM_PROF_ATR_H, s);
@@ -362,7 +347,7 @@ int stage_weights(AdmmCtx* c, int side, hipStream_t s) {
   // 2. trial direction Q = A G (not needed on the fast x side: formed inside the trials)
   if (!(fast && side == 0)) {
     ProfScope ps(c, side == 0 ? ADMM_PROF_QGEMM_X : ADMM_PROF_QGEMM_H, s);
-    if (side == 1 && c->split3) launch_qgemm3(g, c->buf.gates[ADMM_H], c->G, c->gimg, c->Q, s, c->q_pieces, c->qpair, c->qres);
+    if (side == 1 && c->split3) launch_qgemm3(g, c->buf.gates[ADMM_H], c->G, c->gimg, c->Q, s);
     else launch_qgemm(g, side, c->buf.x, c->buf.gates[ADMM_H], c->G, c->Q, s);
   }
   // 3. line search: trial passes of kTrialJ exponents each until every gate has passed
@@ -399,7 +384,7 @@ int stage_weights(AdmmCtx* c, int side, hipStream_t s) {
       if (fast)
         launch_trial_fast(g, side, pass, side == 1 ? zh : c->zc, c->tgt, side == 1 ? c->Q : nullptr, c->buf.x,
                           side == 0 ? c->G : c->dW, c->found + 4 * par, c->tr_part, nblk, s, sx.zx ? &sx : nullptr,
-                          side == 1 && c->split3 ? c->qpair : 0);
+                          side == 1 && c->split3 ? q_layout(g) : 0);
       else
         launch_trial(g, pass, c->zc, c->tgt, c->Q, c->found + 4 * par, c->tr_part, nblk, s);
     }
@@ -532,10 +517,6 @@ int admm_create(const AdmmDims* dims, const AdmmParams* params, int device, Admm
   // kernel-choice knobs live in the context's Geom (a per-context read: tests flip them
   // between contexts of one process)
   if (const char* e = std::getenv("ADMM_SWEEP_R16")) g.r16 = std::atoi(e) != 0;
-  if (const char* e = std::getenv("ADMM_TRIAL_MX")) g.trial_mx = std::atoi(e) != 0;
-  if (const char* e = std::getenv("ADMM_ATR_WIDE")) g.atr_wide = std::atoi(e) != 0;
-  if (const char* e = std::getenv("ADMM_SWEEP_SPLIT"))
-    c->sweep_split = std::max(1, std::min(kMaxSweepStreams, std::atoi(e)));
   c->sweep_rows = sweep_rows_ok(g);
   if (const char* e = std::getenv("ADMM_SWEEP_ROWS")) c->sweep_rows = c->sweep_rows && std::atoi(e) != 0;
   if (const char* e = std::getenv("ADMM_TGT_SWEEP")) c->tgt_sweep = std::atoi(e) != 0;
@@ -546,11 +527,6 @@ int admm_create(const AdmmDims* dims, const AdmmParams* params, int device, Admm
   c->spec_x = fast_path(g) && trial_rows_ok(g);
   if (const char* e = std::getenv("ADMM_SPEC_X")) c->spec_x = c->spec_x && std::atoi(e) != 0;
   if (const char* e = std::getenv("ADMM_SPLIT3")) c->split3 = c->split3 && std::atoi(e) != 0;
-  if (const char* e = std::getenv("ADMM_ATR3W")) c->atr3w = std::atoi(e) != 0;
-  if (const char* e = std::getenv("ADMM_QPAIR")) c->qpair = std::max(0, std::min(2, std::atoi(e)));
-  if (const char* e = std::getenv("ADMM_QRES")) c->qres = std::atoi(e) != 0;
-  if (const char* e = std::getenv("ADMM_Q_PIECES")) c->q_pieces = std::max(1, std::min(3, std::atoi(e)));
-  if (const char* e = std::getenv("ADMM_ATR_PIECES")) c->atr_pieces = std::atoi(e) == 2 ? 2 : 3;
   if (const char* e = std::getenv("ADMM_P16")) c->p16 = std::atoi(e) != 0;
   if (const char* e = std::getenv("ADMM_ATR_F16")) c->atr_f16 = std::atoi(e) != 0;
   Hyper& h = c->hp;

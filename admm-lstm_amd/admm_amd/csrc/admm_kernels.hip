@@ -1880,12 +1880,7 @@ __device__ __forceinline__ void trial_rows_body(const Geom& g, int q, int pass, 
             __builtin_nontemporal_load(reinterpret_cast<const bf16x4*>(Qb + pr * 4 * g.H)), f32x4);
         v.q[0] = f32x2{qq[0], qq[1]};
         v.q[1] = f32x2{qq[2], qq[3]};
-      } else if constexpr (QP == 1) {   // BT % 4 == 0: one quad
-        const int64_t pr = __builtin_amdgcn_readfirstlane((int)((ra < BT ? ra : BT - 4) >> 2));
-        const f32x4 qq = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(Qq + pr * 4 * g.H));
-        v.q[0] = f32x2{qq[0], qq[1]};
-        v.q[1] = f32x2{qq[2], qq[3]};
-      } else {
+      } else {   // row-major f32 (BT % 4 != 0)
 #pragma unroll
         for (int h = 0; h < 2; ++h)
           v.q[h] = f32x2{__builtin_nontemporal_load(Qq + r[2 * h] * g.H), __builtin_nontemporal_load(Qq + r[2 * h + 1] * g.H)};
@@ -2955,7 +2950,7 @@ void launch_sweep_t(const Geom& g, int t, const Weights& w, const Hyper& hp, con
 }
 
 // 16-row tiles for 256 < H <= 512 (ADMM_SWEEP_R16=0: those shapes take the per-t sweep)
-static bool sweep_r16(const Geom& g) { return g.r16 && g.H > 256 && g.H <= 512 && g.H % 64 == 0; }
+static bool sweep_r16(const Geom& g) { return g.r16 && g.H > 256 && g.H <= 512 && g.H % 64 == 0; }  // (r16: test hook)
 
 bool sweep_rows_ok(const Geom& g) {
   // 32-bit buffer offsets: a [B][T+1][H] plane and a [B*T][H] z-cache plane in bytes
@@ -3044,7 +3039,7 @@ void launch_resid(const Geom& g, const Hyper& hp, const ResidArgs& a, hipStream_
   k_resid<<<grid, kThreads, 0, s>>>(g, hp, a);
 }
 
-bool atr_wide(const Geom& g) { return g.atr_wide && g.H % 256 == 0; }
+bool atr_wide(const Geom& g) { return g.H % 256 == 0; }
 
 int atr_splits(const Geom& g, int side) {
   const int Kd = side == 0 ? g.D : g.H;
@@ -3206,9 +3201,9 @@ void launch_apply_fix(const Geom& g, const float* x, const float* dW, const floa
 
 bool trial_rows_ok(const Geom& g) { return g.H % 256 == 0; }
 
-bool trial_mx_ok(const Geom& g) {   // ADMM_TRIAL_MX=0: the x side on k_trial_rows (VALU q)
+bool trial_mx_ok(const Geom& g) {   // else (a gate plane past 2 GB) the x side runs on k_trial_rows (VALU q)
   // 32-bit buffer offsets within one gate plane
-  return g.trial_mx && g.H % 256 == 0 && g.D <= 16 && g.BT() * g.H * 4 < (int64_t)INT32_MAX;
+  return g.H % 256 == 0 && g.D <= 16 && g.BT() * g.H * 4 < (int64_t)INT32_MAX;
 }
 
 void launch_trial_fast(const Geom& g, int side, int pass, const float* zc, const float* tgt, const float* Q,
@@ -3223,8 +3218,6 @@ void launch_trial_fast(const Geom& g, int side, int pass, const float* zc, const
       dim3 gr(nblk, 4, g.H / 256);
       if (qpair == 2 && qpair_ok(g))
         k_trial_rows<1, 4, false, false, 2, TL><<<gr, kThreads, 0, s>>>(g, pass, zc, tgt, Q, x, Wsrc, found, part, nblk, sp);
-      else if (qpair == 1 && qpair_ok(g))
-        k_trial_rows<1, 4, false, false, 1, TL><<<gr, kThreads, 0, s>>>(g, pass, zc, tgt, Q, x, Wsrc, found, part, nblk, sp);
       else
         k_trial_rows<1, 4, false, false, 0, TL><<<gr, kThreads, 0, s>>>(g, pass, zc, tgt, Q, x, Wsrc, found, part, nblk, sp);
       return;

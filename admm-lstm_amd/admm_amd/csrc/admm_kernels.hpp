@@ -42,9 +42,9 @@ struct Geom {
   int64_t Bg;   // global rows (a-update constant)
   int T, D, H, O;
   DivU32 dT{};  // by T; set with set_T() (B*T < 2^31 is checked at create)
-  // kernel-choice knobs, read from the environment once per context (admm_create):
-  // ADMM_SWEEP_R16, ADMM_TRIAL_MX, ADMM_ATR_WIDE
-  bool r16 = true, trial_mx = true, atr_wide = true;
+  // test hook read from the environment once per context (admm_create): ADMM_SWEEP_R16=0 runs
+  // 256 < H <= 512 on the per-t sweep (the path of the other widths) to compare the two
+  bool r16 = true;
   __host__ __device__ int64_t BT() const { return B * (int64_t)T; }
   __host__ __device__ int TP() const { return T + 1; }
   void set_T() { dT = DivU32::make((uint32_t)T); }
@@ -219,32 +219,22 @@ void launch_atr_fused(const Geom& g, const Hyper& hp, const float* x, const floa
 bool split3_ok(const Geom& g);
 size_t split3_gimg_floats(const Geom& g);
 int atr3_splits(const Geom& g);
-// two_waves (H == 256, atr3w_ok): k_atr3w, 8 waves with 128 accumulators (two per SIMD) instead of
-// k_atr3's 4 with 256; the same products in the same order, so bit-identical slabs
-bool atr3w_ok(const Geom& g);
-// range, dW non-null (H % 256 == 0, two_waves): the scaled-fp16 two-way split instead, with the
-// operand ranges the persistent sweep left (SweepT::range, plus [5] = max_row sum_d |x_d|) and the x
-// stage's decided update dW [4][D][H] (k_atr3w<2, true>)
+// range, dW non-null: k_atr3w on scaled-fp16 two-way splits, with the operand ranges the persistent
+// sweep left (SweepT::range, plus [5] = max_row sum_d |x_d|) and the x stage's decided update dW
+// [4][D][H]; else on split3 (both f32-accurate)
 void launch_atr3(const Geom& g, const float* Sh, const float* zc, const float* tgt, float* slab, int nsplit,
-                 hipStream_t s, bool two_waves = true, int pieces = 3, const float* range = nullptr,
-                 const float* dW = nullptr);
+                 hipStream_t s, const float* range = nullptr, const float* dW = nullptr);
 // range[5] = max over rows of sum_d |x[row][d]| (atomicMax into a zeroed slot)
 void launch_x_l1max(const Geom& g, const float* x, float* range, hipStream_t s);
-// pieces = 3: f32-accurate split3 products; 2: two-way splits, three products (~2^-16 relative),
-// enough for the trial direction ("trial direction precision")
-// qpair (and qpair_ok: BT % 4 == 0): Q in the row-quad layout [q][row / 4][j][row % 4] that
-// launch_trial_fast(..., qpair) reads (the h-side trial pass, H % 256 == 0); 1 = f32, 2 = bf16
-// elements (0: row-major f32)
+// Q = Hprev G, the h-side trial direction: Hprev in two bf16 pieces, G rounded to bf16 (it enters
+// only the line-search remainder, DESIGN.md "trial direction precision").  Layout: bf16 row quads
+// [q][row / 4][j][row % 4] when qpair_ok (BT % 4 == 0), else row-major f32 -- launch_trial_fast's
+// qpair argument is q_layout(g).  H = 256 (qres_ok): k_qgemm_res, the G image resident in LDS;
+// otherwise the staged k_qgemm3<1, layout>.
 bool qpair_ok(const Geom& g);
-void launch_qgemm3(const Geom& g, const float* Sh, const float* G, float* gimg, float* Q, hipStream_t s,
-                   int pieces = 3, int qpair = 0, bool qres = false);
-// qres: Q = Hprev G with the gate's G image resident in LDS (k_qgemm_res: H = 256, pieces = 1,
-// qpair = 2; bit-identical to k_qgemm3<1, 2>)
 bool qres_ok(const Geom& g);
-// the two halves of launch_qgemm3: G -> split image, then Q = Hprev G (gates with found[q] set skipped)
-void launch_split_g(const Geom& g, const float* G, float* gimg, hipStream_t s);
-void launch_qgemm3_img(const Geom& g, const float* Sh, const float* gimg, float* Q, const int* found, hipStream_t s,
-                       int pieces = 3, int qpair = 0, bool qres = false);
+int q_layout(const Geom& g);   // 2 (bf16 row quads) or 0 (row-major f32)
+void launch_qgemm3(const Geom& g, const float* Sh, const float* G, float* gimg, float* Q, hipStream_t s);
 // decide the first passing k in this pass's window; on success update the weights
 struct SelectArgs {
   int side;                 // 0 x, 1 h

@@ -1,7 +1,7 @@
 // admm_split3.hip -- the h-stage GEMMs of the weight update on bf16 matrix cores with
 // f32-accurate three-way split operands (admm_dev.hpp split3).
 //
-//   k_atr3   slab[sp][q][m][j] = sum_{rows of split sp} Hprev[row][m] * R_q[row][j]
+//   k_atr3w  slab[sp][q][m][j] = sum_{rows of split sp} Hprev[row][m] * R_q[row][j]
 //            the gradient G_q = rho_q Hprev^T R_q of the h side (admm.py:302-312), with the
 //            residual R_q = (phi(z) - tgt) phi'(z) formed from the z cache and the target while
 //            the tile is staged (R is never materialised);
@@ -51,15 +51,12 @@ __global__ __launch_bounds__(kThreads) void k_split_g(int H, const float* __rest
 // One 128 x 256 tile of one gate per workgroup (qgemm3_tile).  found != nullptr: gates whose
 // line search has already decided are skipped (the later trial passes, when pass 0 ran fused
 // in k_qtrial3 and Q was never formed).
-// QP: Q is written in the row-quad layout Q[q][row / 4][j][row % 4] (BT % 4 == 0): registers
-// 4i .. 4i + 3 of a 32x32 accumulator hold four consecutive rows of one column, so each lane
-// stores 16 B and a wave-instruction two contiguous 512-B runs -- a quarter of the store
-// instructions of the row-major layout (the epilogue is store-issue bound); the h-side trial
-// reads a row pair (rows 2i, 2i + 1: one half of a quad) as one float2.
-// QP = 2: the same row-quad layout in bf16 (Q[q][row / 4][j][row % 4] as bf16x4, 8 B per quad and
-// column): Q only enters the line-search remainder, where its ~2^-9 relative rounding moves the
-// decision quantity by ~2^-8 (DESIGN.md "trial direction precision"); half the bytes written here
-// and read back by the h-side trials.
+// QP = 2: Q is written in the row-quad layout Q[q][row / 4][j][row % 4] of bf16 (BT % 4 == 0):
+// registers 4i .. 4i + 3 of a 32x32 accumulator hold four consecutive rows of one column, so each
+// lane stores 8 B per quad and column -- a quarter of the store instructions of the row-major layout
+// (the epilogue is store-issue bound), and Q only enters the line-search remainder, where its ~2^-9
+// relative rounding moves the decision quantity by ~2^-8 (DESIGN.md "trial direction precision").
+// QP = 0: row-major f32 (the fallback for BT % 4 != 0).
 template <int NP, int QP, int BM>
 __global__ __launch_bounds__(2 * BM) void k_qgemm3(Geom g, const float* __restrict__ Sh,
                                                     const bf16x8* __restrict__ gi, float* __restrict__ Q,
@@ -89,22 +86,6 @@ __global__ __launch_bounds__(2 * BM) void k_qgemm3(Geom g, const float* __restri
           const f32x4 v = f32x4{acc[mi][ni][r], acc[mi][ni][r + 1], acc[mi][ni][r + 2], acc[mi][ni][r + 3]};
           __builtin_nontemporal_store(__builtin_convertvector(v, bf16x4), Qp + (row >> 2) * H + ni * 32);
         }
-      }
-    return;
-  }
-  if constexpr (QP == 1) {
-    f32x4* Qp = reinterpret_cast<f32x4*>(Q + (int64_t)q * BT * H) + Q3_BN * cb + wc * 128 + c32;
-#pragma unroll
-    for (int mi = 0; mi < 2; ++mi)
-#pragma unroll
-      for (int r = 0; r < 16; r += 4) {
-        const int64_t row = m0 + wr * 64 + mi * 32 + acc_row(r, lane);   // a multiple of 4
-        if (row >= BT) continue;
-#pragma unroll
-        for (int ni = 0; ni < 4; ++ni)
-          if (!(S3_ABL & 16) || acc[mi][ni][r] == 12345.f)
-            __builtin_nontemporal_store(f32x4{acc[mi][ni][r], acc[mi][ni][r + 1], acc[mi][ni][r + 2], acc[mi][ni][r + 3]},
-                                        Qp + (row >> 2) * H + ni * 32);
       }
     return;
   }
@@ -246,34 +227,20 @@ __global__ __launch_bounds__(64 * QR_WAVES, 1) void k_qgemm_res(Geom g, const fl
 }
 
 // ------------------------------------------------------------------ slab = Hprev^T R
-// Workgroup: 256 hidden units m x BN columns j of one gate (H % 256 == 0) over the rows of one
-// split, in 16-row steps; 4 waves as 2 (m) x 2 (j) of 128 x BN/2.  BN = 256: 256 accumulators
-// per lane, one workgroup (one wave per SIMD) per CU.  BN = 128: 128 accumulators, 72 KB of LDS,
-// two workgroups per CU so one wave's MFMAs overlap the other's loads and split arithmetic.
-// Both MFMA operands are k(= row)-strided in memory.  Staging keeps rows as they are: a thread
-// loads float4s of whole rows (a wave-instruction = one 1-KB Hprev row, one or two rows of R) and
-// stores the split pieces row-major; the fragments come back transposed through
-// ds_read_b64_tr_b16 (two per piece: rows k..k+3 and k+4..k+7 of 16 columns per lane group).
-// Images: [piece][128-column block][16 rows][128 bf16], 256-B rows whose 16-B chunks are
-// XOR-permuted by the row (cdna_hip_programming.md T10 image (b)): the row-major staging writes
-// and the transposed reads are both conflict-free.  The loads run two steps ahead through a
-// two-slot register ring.
-#ifndef A3_BN_SEL
-#define A3_BN_SEL 256   // 128: two workgroups per CU (measured slower on C3: 1.10 vs 1.05 ms)
-#endif
-constexpr int A3_BM = 256, A3_BN = A3_BN_SEL, A3_KS = 16;
+// Tile: 256 hidden units m x 256 columns j of one gate (H % 256 == 0) over the rows of one split, in
+// 16-row steps.  Both MFMA operands are k(= row)-strided in memory.  Staging keeps rows as they are
+// (a wave-instruction = one 1-KB row) and stores the split pieces row-major; the fragments come back
+// transposed through ds_read_b64_tr_b16 (two per piece: rows k..k+3 and k+4..k+7 of 16 columns per
+// lane group).  Images: [piece][128-column block][16 rows][128 x 16 bit], 256-B rows whose 16-B
+// chunks are XOR-permuted by the row (cdna_hip_programming.md T10 image (b)): the row-major staging
+// writes and the transposed reads are both conflict-free.
+constexpr int A3_BM = 256, A3_BN = 256, A3_KS = 16;
 constexpr int A3_SUB = A3_KS * 128;          // bf16 of one 128-column block (16 rows x 128 columns)
 
 template <int BN>
 struct A3 {
   static constexpr int PA = (A3_BM / 128) * A3_SUB;   // one split piece of the Hprev operand
   static constexpr int PR = (BN / 128) * A3_SUB;      // one split piece of the R operand
-  static constexpr int STAGE = 3 * PA + 3 * PR;
-  static constexpr int LPR = BN / 4;                   // lanes per R row (float4 each)
-  static constexpr int RPI = 64 / LPR;                 // R rows per wave-instruction
-  static constexpr int NR = 4 / RPI;                   // R loads per thread per step
-  static constexpr int NI = BN / 64;                   // 32-column fragments per wave
-  static constexpr int MINB = BN == 128 ? 2 : 1;       // workgroups per CU
 };
 
 __device__ __forceinline__ int a3_off(int row, int col) {   // bf16 offset of (row, col), col % 4 == 0
@@ -281,194 +248,12 @@ __device__ __forceinline__ int a3_off(int row, int col) {   // bf16 offset of (r
   return sub * A3_SUB + row * 128 + 8 * (ch ^ (((row & 3) << 2) | ((row >> 2) & 3))) + (cw & 4);
 }
 
-template <int BN>
-struct Atr3Ring { float4 a[4], z[A3<BN>::NR], t[A3<BN>::NR]; };
-
-template <bool TANH, int BN>
-__device__ __forceinline__ void atr3_body(const Geom& g, int mb, int nb, int q, int sp, int nsplit,
-                                          const float* __restrict__ Sh, const float* __restrict__ zq,
-                                          const float* __restrict__ tq, float* __restrict__ slab, __bf16* img) {
-  using P = A3<BN>;
-  const int H = g.H;
-  const int64_t BT = g.BT();
-  const int64_t per = ((BT + nsplit - 1) / nsplit + A3_KS - 1) / A3_KS * A3_KS;
-  const int64_t r0 = sp * per, r1 = r0 + per < BT ? r0 + per : BT;
-  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  // staging: Hprev columns 4cg..4cg+3 of rows 4rg..4rg+3; R columns 4cz.. of rows
-  // 4rg + RPI i + lh.  rg (the wave) is made provably uniform so the row offsets stay in SGPRs
-  // (no waterfall loops around the buffer loads, guide T20)
-  const int cg = lane, rg = __builtin_amdgcn_readfirstlane(wave);
-  const int lh = lane / P::LPR, cz = lane % P::LPR;
-  const __amdgpu_buffer_rsrc_t rA = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(Sh), 0,
-                                                                      (int)(g.B * g.TP() * H * 4), kBufWord3);
-  const __amdgpu_buffer_rsrc_t rZ = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(zq), 0, (int)(BT * H * 4), kBufWord3);
-  const __amdgpu_buffer_rsrc_t rT = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(tq), 0, (int)(BT * H * 4), kBufWord3);
-  const int va = (mb * A3_BM + 4 * cg) * 4, vz = (nb * BN + 4 * cz) * 4;
-  // rows past r1 are loaded clamped (branch-free) and meet R = 0 in put()
-  auto gload = [&](Atr3Ring<BN>& R, int64_t k0) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int64_t r = k0 + 4 * rg + i, row = r < r1 ? r : r1 - 1;
-      const int sa = (int)(g.hrow(row) * H * 4);
-      R.a[i] = (S3_ABL & 1) ? make_float4(i, 1, 2, 3)
-                            : __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rA, va, sa, 0));
-    }
-#pragma unroll
-    for (int i = 0; i < P::NR; ++i) {
-      int vo = vz, so = 0;
-      if constexpr (P::RPI == 1) {
-        const int64_t r = k0 + 4 * rg + i, row = r < r1 ? r : r1 - 1;
-        so = (int)(row * H * 4);
-      } else {   // the row depends on the lane: the offset goes into the VGPR
-        const int64_t r = k0 + 4 * rg + P::RPI * i + lh, row = r < r1 ? r : r1 - 1;
-        vo += (int)row * H * 4;
-      }
-      R.z[i] = (S3_ABL & 2) ? make_float4(0.1f, 0.2f, 0.3f, 0.4f)
-                            : __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rZ, vo, so, 2));
-      R.t[i] = (S3_ABL & 2) ? make_float4(0.5f, 0.5f, 0.5f, 0.5f)
-                            : __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rT, vo, so, 2));
-    }
-  };
-  // split a ring slot (4 columns of 4 Hprev rows and of NR R rows) into the images of stage st
-  auto put = [&](int st, const Atr3Ring<BN>& R, int64_t k0) {
-    __bf16* A = img + st * P::STAGE;
-    __bf16* B = A + 3 * P::PA;
-    bf16x4 p0, p1, p2;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int o = a3_off(4 * rg + i, 4 * cg);
-      split3(f32x4{R.a[i].x, R.a[i].y, R.a[i].z, R.a[i].w}, p0, p1, p2);
-      *reinterpret_cast<bf16x4*>(A + o) = p0;
-      *reinterpret_cast<bf16x4*>(A + P::PA + o) = p1;
-      *reinterpret_cast<bf16x4*>(A + 2 * P::PA + o) = p2;
-    }
-#pragma unroll
-    for (int i = 0; i < P::NR; ++i) {
-      const int rr = 4 * rg + P::RPI * i + lh;
-      const int o = a3_off(rr, 4 * cz);
-      const bool ok = k0 + rr < r1;
-      const float zz[4] = {R.z[i].x, R.z[i].y, R.z[i].z, R.z[i].w};
-      const float tt[4] = {R.t[i].x, R.t[i].y, R.t[i].z, R.t[i].w};
-      f32x4 rv;
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        float phi, dphi;
-        phi_fast<TANH>(zz[u], phi, dphi);
-        rv[u] = ok ? (phi - tt[u]) * dphi : 0.f;
-      }
-      split3(rv, p0, p1, p2);
-      *reinterpret_cast<bf16x4*>(B + o) = p0;
-      *reinterpret_cast<bf16x4*>(B + P::PR + o) = p1;
-      *reinterpret_cast<bf16x4*>(B + 2 * P::PR + o) = p2;
-    }
-  };
-  // transposed fragment reads: lane group gi = lane >> 4 takes columns +16 (gi & 1) and rows
-  // 8 (gi >> 1) .. +7; lane 4qq + pp of a group addresses row qq (+4 for the second read),
-  // columns 4pp..4pp+3
-  const int gi = lane >> 4, qq = (lane >> 2) & 3, pp = lane & 3;
-  const int frow = 8 * (gi >> 1) + qq, fcol = 16 * (gi & 1) + 4 * pp;
-  auto frag = [&](const __bf16* O, int piece, int cbase, bf16x8 (&f)[3]) {
-    const int o0 = a3_off(frow, cbase + fcol), o1 = a3_off(frow + 4, cbase + fcol);
-#pragma unroll
-    for (int p = 0; p < 3; ++p) {
-      typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
-      const bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(O + p * piece + o0));
-      const bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(O + p * piece + o1));
-      f[p] = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-    }
-  };
-  const int wr = wave >> 1, wc = wave & 1;
-  f32x16 acc[4][P::NI];
-  zero_acc(acc);
-  auto compute = [&](int st) {
-    const __bf16* A = img + st * P::STAGE;
-    const __bf16* B = A + 3 * P::PA;
-    bf16x8 b[P::NI][3];
-#pragma unroll
-    for (int ni = 0; ni < P::NI; ++ni) frag(B, P::PR, wc * (BN / 2) + ni * 32, b[ni]);
-#pragma unroll
-    for (int mi = 0; mi < 4; ++mi) {
-      bf16x8 a[3];
-      frag(A, P::PA, wr * 128 + mi * 32, a);
-#pragma unroll
-      for (int ni = 0; ni < P::NI; ++ni) {
-        if (S3_ABL & 4) acc[mi][ni][0] += (float)a[0][0] * (float)b[ni][0][0];
-        else acc[mi][ni] = mfma_split3(a, b[ni], acc[mi][ni]);
-      }
-    }
-  };
-  if (r0 >= r1) {
-  } else if constexpr (P::MINB == 1) {
-    Atr3Ring<BN> R0, R1;
-    gload(R0, r0);
-    gload(R1, r0 + A3_KS);
-    put(0, R0, r0);
-    __syncthreads();
-    // iteration of step s: issue step s+2 into the free slot, MFMAs of step s, split step s+1
-    // into the other image.  Steps in pairs; an odd count runs one all-masked step (R = 0).
-    for (int64_t k0 = r0; k0 < r1; k0 += 2 * A3_KS) {
-      gload(R0, k0 + 2 * A3_KS);
-      compute(0);
-      put(1, R1, k0 + A3_KS);
-      __syncthreads();
-      gload(R1, k0 + 3 * A3_KS);
-      compute(1);
-      put(0, R0, k0 + 2 * A3_KS);
-      __syncthreads();
-    }
-  } else {
-    // two workgroups per CU: a one-slot ring (step s+1 in flight during the MFMAs of step s);
-    // the other workgroup covers the rest of the load latency
-    Atr3Ring<BN> R0;
-    gload(R0, r0);
-    put(0, R0, r0);
-    __syncthreads();
-    int st = 0;
-    for (int64_t k0 = r0; k0 < r1; k0 += A3_KS) {
-      gload(R0, k0 + A3_KS);
-      compute(st);
-      put(st ^ 1, R0, k0 + A3_KS);
-      __syncthreads();
-      st ^= 1;
-    }
-  }
-  float* out = slab + ((int64_t)sp * 4 + q) * H * H + nb * BN + wc * (BN / 2) + (lane & 31);
-#pragma unroll
-  for (int mi = 0; mi < 4; ++mi)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int m = mb * A3_BM + wr * 128 + mi * 32 + acc_row(r, lane);
-#pragma unroll
-      for (int ni = 0; ni < P::NI; ++ni) out[(int64_t)m * H + ni * 32] = acc[mi][ni][r];
-    }
-}
-
-__global__ __launch_bounds__(kThreads, A3<A3_BN>::MINB) void k_atr3(Geom g, const float* __restrict__ Sh,
-                                                                     const float* __restrict__ zc,
-                                                                     const float* __restrict__ tgt,
-                                                                     float* __restrict__ slab, int nsplit) {
-  __shared__ __attribute__((aligned(16))) __bf16 img[2 * A3<A3_BN>::STAGE];
-  const int nmb = g.H / A3_BM, nnb = g.H / A3_BN;
-  int lid = xcd_swizzle(blockIdx.x, gridDim.x);
-  const int q = lid % 4;          // the 4 gates of one split share the Hprev rows: same XCD
-  lid /= 4;
-  const int mb = lid % nmb;
-  lid /= nmb;
-  const int nb = lid % nnb, sp = lid / nnb;
-  const int64_t n = g.BT() * g.H;
-  if (q == 2)
-    atr3_body<true, A3_BN>(g, mb, nb, q, sp, nsplit, Sh, zc + q * n, tgt + q * n, slab, img);
-  else
-    atr3_body<false, A3_BN>(g, mb, nb, q, sp, nsplit, Sh, zc + q * n, tgt + q * n, slab, img);
-}
-
-// ------------------------------------------------------------------ slab = Hprev^T R, two waves per SIMD
-// The same tile, images and fragment reads as k_atr3 (256 m x 256 j of one gate, 16-row steps),
-// but 8 waves as 2 (m) x 4 (j) of 128 x 64: 128 accumulators per lane, so two waves share each
-// SIMD and one wave's staging VALU (phi, phi', the split3 of R and Hprev) and waits issue while
-// the other's MFMAs run.  At one wave per SIMD (k_atr3) the staging and the MFMAs of a wave
-// serialise.  Each wave stages two rows of each operand per step (one 1-KB row per
-// wave-instruction), two steps ahead through a two-slot register ring.
+// k_atr3w: 8 waves as 2 (m) x 4 (j) of 128 x 64: 128 accumulators per lane, so two waves share each
+// SIMD and one wave's staging VALU (phi, phi', the split of R and Hprev) and waits issue while the
+// other's MFMAs run (at one wave per SIMD with 256 accumulators -- round 2's k_atr3 -- the staging
+// and the MFMAs of a wave serialised: 0.85 against 0.80 ms at C3).  Each wave stages two rows of
+// each operand per step (one 1-KB row per wave-instruction), two steps ahead through a two-slot
+// register ring.
 constexpr int A3W_THREADS = 512;
 #ifndef A3W_ABL
 #define A3W_ABL 0   // timing ablations for tools/build_lib_variant.sh: 1 no loads, 2 no MFMAs
@@ -476,11 +261,10 @@ constexpr int A3W_THREADS = 512;
 struct Atr3wRing { float4 a[2], z[2], t[2]; };
 
 // (mb, nb): the 256 x 256 block of G_q (H_prev columns 256 mb.., R columns 256 nb..).
-// NP = 3: split3 operands, six products (f32-accurate); NP = 2: two-way splits, the three
-// products of mfma_split2 (~2^-16 relative per product, the accuracy of the reference's own fp32
-// sums over B*T rows; DESIGN.md "h-side gradient on two-way splits"), half the matrix work and
-// two thirds of the staging
-// F16 (NP = 2): the two pieces are fp16 instead of bf16 (hi = rn(a), lo = rn(a - hi): 22 bits,
+// NP = 3: split3 operands, six products (f32-accurate); the first h stage after the state is bound
+// or invalidated (no sweep has bounded the operands yet).
+// NP = 2, F16: two fp16 pieces instead (bf16 two-way splits, ~2^-16 per product, measured 1.3-3.7x
+// the error of a torch fp32 GEMM of the same operands and were dropped in round 4) (hi = rn(a), lo = rn(a - hi): 22 bits,
 // ~2^-22 relative per piece pair, 2^-20.4 per product at worst -- f32-accurate once summed with the
 // f32 accumulation of thousands of rows), on the same matrix rate (v_mfma_f32_32x32x16_f16).  fp16
 // has 5 exponent bits, so both operands are first scaled by exact powers of two that put their
@@ -574,8 +358,7 @@ __device__ __forceinline__ void atr3w_body(const Geom& g, int q, int sp, int nsp
     bf16x4 p0, p1, p2;
     auto pieces = [&](f32x4 v) {
       if constexpr (F16) split2h(v, p0, p1);
-      else if constexpr (NP == 3) split3(v, p0, p1, p2);
-      else split2(v, p0, p1);
+      else split3(v, p0, p1, p2);
     };
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
@@ -603,7 +386,8 @@ __device__ __forceinline__ void atr3w_body(const Geom& g, int q, int sp, int nsp
       if constexpr (NP == 3) *reinterpret_cast<bf16x4*>(B + 2 * P::PR + o) = p2;
     }
   };
-  // transposed fragment reads (k_atr3's lane map)
+  // transposed fragment reads: lane group gi = lane >> 4 takes columns +16 (gi & 1) and rows
+  // 8 (gi >> 1) .. +7; lane 4qq + pp of a group addresses row qq (+4 for the second read), columns 4pp..4pp+3
   const int gi = lane >> 4, qq = (lane >> 2) & 3, pp = lane & 3;
   const int frow = 8 * (gi >> 1) + qq, fcol = 16 * (gi & 1) + 4 * pp;
   auto frag = [&](const __bf16* O, int piece, int cbase, bf16x8 (&f)[3]) {
@@ -633,8 +417,7 @@ __device__ __forceinline__ void atr3w_body(const Geom& g, int q, int sp, int nsp
       for (int ni = 0; ni < 2; ++ni) {
         if (A3W_ABL & 2) acc[mi][ni][0] += (float)a[0][0] * (float)b[ni][0][0];   // ablation: no MFMAs
         else if constexpr (F16) acc[mi][ni] = mfma_split2h(a, b[ni], acc[mi][ni]);
-        else if constexpr (NP == 3) acc[mi][ni] = mfma_split3(a, b[ni], acc[mi][ni]);
-        else acc[mi][ni] = mfma_split2(a, b[ni], acc[mi][ni]);
+        else acc[mi][ni] = mfma_split3(a, b[ni], acc[mi][ni]);
       }
     }
   };
@@ -697,26 +480,20 @@ size_t split3_gimg_floats(const Geom& g) { return (size_t)4 * g.H * g.H * 3 / 2;
 
 int atr3_splits(const Geom& g) {
   const int tiles = (g.H / A3_BM) * (g.H / A3_BN) * 4;
-  int ns = 256 * A3<A3_BN>::MINB / tiles;   // one resident wave of workgroups
+  int ns = 256 / tiles;   // one resident wave of workgroups (one per CU)
   const int64_t max_by_rows = g.BT() / 256;
   if (ns > max_by_rows) ns = (int)max_by_rows;
   return ns < 1 ? 1 : ns;
 }
 
-bool atr3w_ok(const Geom& g) { return g.H % 256 == 0; }
-
 void launch_atr3(const Geom& g, const float* Sh, const float* zc, const float* tgt, float* slab, int nsplit,
-                 hipStream_t s, bool two_waves, int pieces, const float* range, const float* dW) {
-  dim3 grid((g.H / A3_BM) * (g.H / A3_BN) * 4 * nsplit);
-  if (two_waves && atr3w_ok(g)) {   // 256 x 256 blocks of each gate's G, nsplit row ranges
-    const int nt = g.H / 256, nb = 4 * nt * nt * nsplit;
-    if (range && dW)   // scaled fp16 two-way splits (f32-accurate, the cost of pieces == 2)
-      k_atr3w<2, true><<<nb, A3W_THREADS, 0, s>>>(g, Sh, zc, tgt, slab, nsplit, range, dW);
-    else if (pieces == 2) k_atr3w<2><<<nb, A3W_THREADS, 0, s>>>(g, Sh, zc, tgt, slab, nsplit, nullptr, nullptr);
-    else k_atr3w<3><<<nb, A3W_THREADS, 0, s>>>(g, Sh, zc, tgt, slab, nsplit, nullptr, nullptr);
-  } else {
-    k_atr3<<<grid, kThreads, 0, s>>>(g, Sh, zc, tgt, slab, nsplit);
-  }
+                 hipStream_t s, const float* range, const float* dW) {
+  // 256 x 256 blocks of each gate's G (H % 256 == 0, split3_ok), nsplit row ranges
+  const int nt = g.H / 256, nb = 4 * nt * nt * nsplit;
+  if (range && dW)   // scaled fp16 two-way splits: f32-accurate at two pieces' matrix work
+    k_atr3w<2, true><<<nb, A3W_THREADS, 0, s>>>(g, Sh, zc, tgt, slab, nsplit, range, dW);
+  else
+    k_atr3w<3><<<nb, A3W_THREADS, 0, s>>>(g, Sh, zc, tgt, slab, nsplit, nullptr, nullptr);
 }
 
 void launch_split_g(const Geom& g, const float* G, float* gimg, hipStream_t s) {
@@ -728,39 +505,19 @@ bool qpair_ok(const Geom& g) { return g.BT() % 4 == 0; }
 
 bool qres_ok(const Geom& g) { return g.H == 256 && qpair_ok(g) && g.BT() * 256 * 2 < (int64_t)INT32_MAX; }
 
-void launch_qgemm3_img(const Geom& g, const float* Sh, const float* gimg, float* Q, const int* found, hipStream_t s,
-                       int pieces, int qpair, bool qres) {
-  // 128-row tiles, two workgroups per CU.  Q3_BM2=256 (8 waves, half the G-image reads per Q row)
-  // measured slower at C3: 0.54 against 0.48 ms -- the two independent workgroups of a CU drift
-  // out of phase, one staging while the other multiplies, where one workgroup's barriers keep
-  // its waves in step.  (The six-product mode needs 272 registers: one wave per SIMD, 128 rows.)
-#ifndef Q3_BM2
-#define Q3_BM2 128
-#endif
+int q_layout(const Geom& g) { return qpair_ok(g) ? 2 : 0; }
+
+void launch_qgemm3(const Geom& g, const float* Sh, const float* G, float* gimg, float* Q, hipStream_t s) {
+  launch_split_g(g, G, gimg, s);
   const bf16x8* gb = reinterpret_cast<const bf16x8*>(gimg);
-  const int qp = qpair_ok(g) ? qpair : 0;
-  if (qres && pieces == 1 && qp == 2 && qres_ok(g)) {   // G resident in LDS: one workgroup per CU
-    k_qgemm_res<<<256, 64 * QR_WAVES, 0, s>>>(g, Sh, gb, Q, found);
+  if (qres_ok(g)) {   // G resident in LDS: one workgroup per CU
+    k_qgemm_res<<<256, 64 * QR_WAVES, 0, s>>>(g, Sh, gb, Q, nullptr);
     return;
   }
-  const int BM = pieces == 2 ? Q3_BM2 : 128;   // (pieces 1: 128)
-  const int64_t nrt = (g.BT() + BM - 1) / BM;
-  dim3 grid((unsigned)(nrt * 4 * (g.H / Q3_BN)));
-  auto go = [&](auto qpm) {
-    constexpr int QPM = decltype(qpm)::value;
-    if (pieces == 1) k_qgemm3<1, QPM, 128><<<grid, 256, 0, s>>>(g, Sh, gb, Q, found);
-    else if (pieces == 2) k_qgemm3<2, QPM, Q3_BM2><<<grid, 2 * Q3_BM2, 0, s>>>(g, Sh, gb, Q, found);
-    else k_qgemm3<3, QPM, 128><<<grid, 256, 0, s>>>(g, Sh, gb, Q, found);
-  };
-  if (qp == 2) go(std::integral_constant<int, 2>{});
-  else if (qp == 1) go(std::integral_constant<int, 1>{});
-  else go(std::integral_constant<int, 0>{});
-}
-
-void launch_qgemm3(const Geom& g, const float* Sh, const float* G, float* gimg, float* Q, hipStream_t s, int pieces,
-                   int qpair, bool qres) {
-  launch_split_g(g, G, gimg, s);
-  launch_qgemm3_img(g, Sh, gimg, Q, nullptr, s, pieces, qpair, qres);
+  // 128-row tiles, two workgroups per CU
+  dim3 grid((unsigned)((g.BT() + 127) / 128 * 4 * (g.H / Q3_BN)));
+  if (q_layout(g) == 2) k_qgemm3<1, 2, 128><<<grid, 256, 0, s>>>(g, Sh, gb, Q, nullptr);
+  else k_qgemm3<1, 0, 128><<<grid, 256, 0, s>>>(g, Sh, gb, Q, nullptr);
 }
 
 }  // namespace admm

@@ -17,7 +17,6 @@ generator + sha256).  Checks per step, through the C ABI:
   agrees -- except searches whose gradient is exactly zero on the GPU (step 1's x side: the stored
   gates are phi(z) bit for bit, so k = 0 as in the reference, while fp64 sees the fp32 rounding of
   the state as a gradient);
-* C3 only: ADMM_Q_PIECES=3 (f32-accurate trial direction) gives a bitwise-identical run.
 
 The fixture also holds the fp64 oracle's exponents from the REFERENCE's own state before every
 step: the test records (and DESIGN.md section 2 cites) how often the reference's fp32 decision
@@ -149,7 +148,7 @@ def _write(name, recs, g):
 
 
 @pytest.mark.parametrize('name', COMPACT)
-def test_fullsize_matches_reference(name, dev, monkeypatch):
+def test_fullsize_matches_reference(name, dev):
     g = Golden(name)
     mods = _load_mods()
     recs = _run(g, mods, dev, arbitrate='all' if name == 'c3' else 'lazy')
@@ -172,14 +171,6 @@ def test_fullsize_matches_reference(name, dev, monkeypatch):
             assert a == k64 or (margin < tie and abs(a - k64) <= 1), (s, i, r['k'], r['ref_k'], r['fp64'],
                                                                         r['g_rel_diff'])
     _check_follows_fp64(recs)
-    if name == 'c3':   # the trial direction on f32-accurate split3 products: the same run bit for bit
-        monkeypatch.setenv('ADMM_Q_PIECES', '3')
-        model, opt = _optimizer(g, mods, dev)
-        for r in recs:
-            opt.step()
-            assert list(opt.last_step_stats()['k'].values()) == r['k'], r['step']
-            for n, p in model.named_parameters():
-                assert torch.equal(p.detach(), r['weights'][n]), (r['step'], n)
 
 
 def _check_follows_fp64(recs):

@@ -83,12 +83,8 @@ int main(int argc, char** argv) {
     float* Q3; (void)hipMalloc(&Q3, (size_t)4 * n * 4);
     timeit("atr3 (split bf16)", f4 * (2 * 4 * n + BT * g.H), 2.0 * BT * g.H * 4 * g.H,
            [&] { launch_atr3(g, S.p[5], zc, tgt, slab3, ns3, s); });
-    timeit("atr3 (1 wave/SIMD)", f4 * (2 * 4 * n + BT * g.H), 2.0 * BT * g.H * 4 * g.H,
-           [&] { launch_atr3(g, S.p[5], zc, tgt, slab3, ns3, s, false); });
     timeit("qgemm3 (split bf16)", f4 * (4 * n + BT * g.H), 2.0 * BT * g.H * 4 * g.H,
            [&] { launch_qgemm3(g, S.p[5], G, gimg, Q3, s); });
-    timeit("qgemm3 (2 pieces)", f4 * (4 * n + BT * g.H), 2.0 * BT * g.H * 4 * g.H,
-           [&] { launch_qgemm3(g, S.p[5], G, gimg, Q3, s, 2); });
     launch_atr_fused(g, hp, x, S.p[5], zc, tgt, dW, slab, atr_splits(g, 1), s);
     launch_qgemm(g, 1, x, S.p[5], G, Q, s);
     (void)hipDeviceSynchronize();
@@ -115,32 +111,11 @@ int main(int argc, char** argv) {
   };
   const std::string mode = argc > 2 ? argv[2] : "";
   if (mode == "s3") { run_s3(); return 0; }
-  if (mode == "q") {   // Q = Hprev G, one-piece G, bf16 row quads: staged k_qgemm3 vs G resident in LDS
+  if (mode == "q") {   // Q = Hprev G (k_qgemm_res at H = 256, else k_qgemm3<1>)
     float* gimg; (void)hipMalloc(&gimg, split3_gimg_floats(g) * 4);
     float* Q3; (void)hipMalloc(&Q3, (size_t)4 * n * 4);
-    launch_split_g(g, G, gimg, s);
     const double qb = f4 * BT * g.H + 2.0 * 4 * n, qf = 2.0 * 2 * BT * g.H * 4 * g.H;
-    for (int r = 0; r < 3; ++r) {
-      timeit("qgemm3<1,2>", qb, qf, [&] { launch_qgemm3_img(g, S.p[5], gimg, Q3, nullptr, s, 1, 2, false); });
-      timeit("qgemm_res", qb, qf, [&] { launch_qgemm3_img(g, S.p[5], gimg, Q3, nullptr, s, 1, 2, true); });
-    }
-    timeit("split_g", 0, 0, [&] { launch_split_g(g, G, gimg, s); });
-    {   // Q of the two kernels (bf16 row quads): identical unless the k order differs (QR_KPERM)
-      float* Q4; (void)hipMalloc(&Q4, (size_t)4 * n * 4);
-      launch_qgemm3_img(g, S.p[5], gimg, Q3, nullptr, s, 1, 2, false);
-      launch_qgemm3_img(g, S.p[5], gimg, Q4, nullptr, s, 1, 2, true);
-      (void)hipDeviceSynchronize();
-      std::vector<uint16_t> a(2 * n * 4 / 2), b(a.size());
-      (void)hipMemcpy(a.data(), Q3, a.size() * 2, hipMemcpyDeviceToHost);
-      (void)hipMemcpy(b.data(), Q4, b.size() * 2, hipMemcpyDeviceToHost);
-      auto f = [](uint16_t h) { uint32_t u = (uint32_t)h << 16; float x; memcpy(&x, &u, 4); return x; };
-      double md = 0, mx = 0; size_t neq = 0;
-      for (size_t i = 0; i < a.size(); ++i) {
-        md = std::max(md, (double)std::fabs(f(a[i]) - f(b[i]))); mx = std::max(mx, (double)std::fabs(f(a[i])));
-        neq += a[i] != b[i];
-      }
-      printf("qgemm_res vs qgemm3: %zu of %zu bf16 differ, max |diff| %.3e (max |Q| %.3e)\n", neq, a.size(), md, mx);
-    }
+    for (int r = 0; r < 3; ++r) timeit("qgemm3", qb, qf, [&] { launch_qgemm3(g, S.p[5], G, gimg, Q3, s); });
     return 0;
   }
   timeit("apply_dwx", 2 * f4 * 4 * n + f4 * BT * g.D, 0, [&] { launch_apply_dwx(g, x, dW, zc, s); });

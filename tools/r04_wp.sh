@@ -13,5 +13,5 @@ run() {   # tag, env...
   tail -3 "$OUT/wp_$tag.log"
   [ $rc -le 1 ] || { echo "stop: rc $rc"; exit $rc; }
 }
-run p2 ADMM_ATR_PIECES=2
-run p3 ADMM_ATR_PIECES=3
+run f16 ADMM_ATR_F16=1
+run s3 ADMM_ATR_F16=0

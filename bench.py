@@ -6,16 +6,20 @@ scaling".  One *step* = one ``step()`` (admm.py:62-78) over the synthetic unifor
 regression problem of SURVEY.md 8(d) (config C3: B=8192, T=32, D=16, H=256, O=1,
 GoogleStock rho/beta), fp32, inputs and state resident in HBM before timing.
 
-Multi-GPU (``torchrun --nproc-per-node N``): one process per GPU, weak scaling --
-every rank owns 8192 samples (C4 at N=8: global batch 65536); the step's batch sums are
-all-reduced with RCCL inside libadmmlstm.so.  ``value`` is the whole-job throughput in
-headline units: batch-8192 ADMM iterations per second = (global_batch / 8192) x it/s
-of the global problem (= it/s at N=1).
+Multi-GPU (``torchrun --nproc-per-node N``): one process per GPU, the step's batch sums
+all-reduced with RCCL inside libadmmlstm.so.  ``value`` is STRONG scaling by default: the
+global batch stays the config's (8192 at C3), each rank steps 8192/N rows, and ``value`` is the
+it/s of that global problem.  A second, weak-scaling measurement (8192 rows per rank, the C4
+shape at N = 8) is reported beside it under ``weak`` ({global_batch, it_s, value in batch-8192
+units = it/s x global_batch / 8192}); ``--scaling weak`` makes that the headline instead.
 
 Also reported (rank 0):
 * ``roofline`` for the dominant kernel class of the timed region, timed live with
   hipEvents on the step's stream (admm_profile); algorithmic bytes/flops per launch
   are those of DESIGN.md "Roofline accounting";
+* ``step_roofline``: the whole step against SURVEY.md 8(d)'s t_roof (GEMMs at the fp32 matrix
+  peak) and against ``t_roof_built`` (the GEMMs priced at the bf16/fp16 matrix rate of the split
+  products they run as, DESIGN.md section 7), with ``step_frac`` / ``step_frac_built``;
 * ``cpu_baseline``: the CPU oracle (a port of the reference op structure, see
   oracle/admm_oracle.py) timed on this host on a bounded sample (N=1 only).
 """
@@ -49,6 +53,8 @@ CONFIGS = {
     'c5': (4096, 64, 1, 512, 'no_dual_y', 'rw'),
     # diagnostic: C4's global batch on one GPU (the line-search exponents of the 8-GPU run)
     'c4g': (65536, 32, 16, 256, 'admm', 'uniform'),
+    # strong-scaling rank of C3 at N = 8: 1024 of the 8192 samples (the per-rank step of the 8-GPU run)
+    'c3s': (1024, 32, 16, 256, 'admm', 'uniform'),
 }
 
 
@@ -92,6 +98,28 @@ def step_roofline_s(B: int, T: int, D: int, H: int) -> float:
     """t_roof = sum over the two phases of max(F / fp32 MFMA peak, B / HBM peak) (SURVEY.md 8(d);
     3.77 ms at C3)."""
     return sum(max(f / PEAK_FP32_MFMA, b / PEAK_HBM) for f, b in survey_terms(B, T, D, H))
+
+
+# The GEMMs as built (DESIGN.md sections 4 and 7): (flops of one f32 GEMM, bf16/fp16 products per
+# f32 product, peak) per step at (B, T, D, H).  Sweep: split3 (6 bf16 products); h-side gradient:
+# scaled fp16 two-way splits (3 products); h-side trial direction: two-piece Hprev x one-piece G
+# (2 products); x side (G_x in the sweep, q = X G_x and X dWx in the trials): f32 MFMA.
+def built_gemms(B: int, T: int, D: int, H: int):
+    gh = 2.0 * B * T * H * 4 * H
+    gx = 2.0 * B * T * D * 4 * H
+    return {'sweep': [(T * 2.0 * B * (D + H) * 4 * H, 6, PEAK_BF16_MFMA)],
+            'weights': [(gh, 3, PEAK_BF16_MFMA), (gh, 2, PEAK_BF16_MFMA), (3 * gx, 1, PEAK_FP32_MFMA)]}
+
+
+def step_roofline_built_s(B: int, T: int, D: int, H: int) -> float:
+    """t_roof with the GEMMs priced as they run: sum over the two phases of max(sum of product
+    work / its matrix peak, SURVEY.md 8(d)'s algorithmic bytes / 8 TB/s) (2.49 ms at C3)."""
+    (_, bw), (_, bb) = survey_terms(B, T, D, H)
+    g = built_gemms(B, T, D, H)
+    t = 0.0
+    for phase, byts in (('weights', bw), ('sweep', bb)):
+        t += max(sum(f * n / peak for f, n, peak in g[phase]), byts / PEAK_HBM)
+    return t
 
 
 def roofline_terms(cls: str, B: int, T: int, D: int, H: int):
@@ -243,7 +271,9 @@ def main():
     ap.add_argument('--steps', type=int, default=20)
     ap.add_argument('--warmup', type=int, default=5)
     ap.add_argument('--config', default='c3', choices=sorted(CONFIGS))
-    ap.add_argument('--scaling', default='weak', choices=['weak', 'strong'])
+    ap.add_argument('--scaling', default='strong', choices=['weak', 'strong'],
+                    help='headline at N > 1: strong (the config global batch, default) or weak (its batch per rank)')
+    ap.add_argument('--no-weak', action='store_true', help='N > 1: skip the extra weak-scaling measurement')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--cpu-steps', type=int, default=3, help='timed CPU-baseline steps after step 1 (median)')
     ap.add_argument('--profile-classes', default='sweep,trial,trial_h,trial_extra,atr_x,atr_h,qgemm_x,qgemm_h,resid,small')
@@ -252,6 +282,10 @@ def main():
     ap.add_argument('--dist-backend', default='nccl', choices=['nccl', 'gloo'])
     ap.add_argument('--one-device', action='store_true', help='all ranks on cuda:0 (rehearsal only)')
     args = ap.parse_args()
+    if args.one_device and args.dist_backend == 'nccl':   # RCCL refuses two ranks on one GPU
+        print('--one-device runs every rank on cuda:0: using --dist-backend gloo (host-staged all-reduces)',
+              file=sys.stderr)
+        args.dist_backend = 'gloo'
 
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))
@@ -282,12 +316,6 @@ def main():
         mod = admm
 
     B, T, D, H, variant, gen = CONFIGS[args.config]
-    Bg = B * world if args.scaling == 'weak' else B
-    per = Bg // world
-    x_all, y_all = make_data(gen, Bg, T, D)
-    x = x_all[rank * per:(rank + 1) * per].contiguous().to(dev)
-    y = y_all[rank * per:(rank + 1) * per].contiguous().to(dev)
-    del x_all, y_all
 
     def barrier():
         torch.cuda.synchronize(dev)
@@ -295,50 +323,75 @@ def main():
             dist.barrier()
         torch.cuda.synchronize(dev)
 
-    def fresh():
-        torch.manual_seed(0)
-        m = LSTM(D, H, 1).to(dev)
-        o = mod.ADMMBasedOptimizer(m, (x, y), example_parameter_dictionary['GoogleStock'], verbose=False,
-                                   distributed=world > 1)
-        for _ in range(args.warmup):
-            o.step()
-        barrier()
-        return m, o
-
-    # kernel classes: hipEvent pairs around each class on the step's stream over the steps the
-    # timed run below takes (same seed and data: the same trajectory); the event records cost
-    # about 0.2 ms per step, so this run is not the timed one
-    classes = [c for c in args.profile_classes.split(',') if c]
-    model, opt = fresh()
-    opt.profile(classes)
-    for _ in range(args.steps):
-        opt.step()
-    barrier()
-    opt.profile(())
-    prof = opt.profile_read()
-    del opt, model
-    torch.cuda.empty_cache()
-    # timed region: plain steps, no events between the launches
-    model, opt = fresh()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        opt.step()
-    barrier()
-    elapsed = time.perf_counter() - t0
     cdev = dev if args.dist_backend == 'nccl' else torch.device('cpu')
-    if dist is not None:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=cdev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-    stats = opt.last_step_stats()
-    loss = float(torch.nn.functional.mse_loss(model(x), y))
-    if dist is not None:
-        lt = torch.tensor([loss * per], dtype=torch.float64, device=cdev)
-        dist.all_reduce(lt)
-        loss = float(lt.item()) / Bg
+
+    def measure(Bg: int, with_profile: bool):
+        """Warm up, (optionally) profile the kernel classes, then time exactly args.steps steps of the
+        global problem of Bg samples, each rank stepping its contiguous row block of Bg / world."""
+        per = Bg // world
+        x_all, y_all = make_data(gen, Bg, T, D)
+        x = x_all[rank * per:(rank + 1) * per].contiguous().to(dev)
+        y = y_all[rank * per:(rank + 1) * per].contiguous().to(dev)
+        del x_all, y_all
+
+        def fresh():
+            torch.manual_seed(0)
+            m = LSTM(D, H, 1).to(dev)
+            o = mod.ADMMBasedOptimizer(m, (x, y), example_parameter_dictionary['GoogleStock'], verbose=False,
+                                       distributed=world > 1)
+            for _ in range(args.warmup):
+                o.step()
+            barrier()
+            return m, o
+
+        prof = {}
+        if with_profile:
+            # kernel classes: hipEvent pairs around each class on the step's stream over the steps the
+            # timed run below takes (same seed and data: the same trajectory); the event records cost
+            # about 0.2 ms per step, so this run is not the timed one
+            classes = [c for c in args.profile_classes.split(',') if c]
+            model, opt = fresh()
+            opt.profile(classes)
+            for _ in range(args.steps):
+                opt.step()
+            barrier()
+            opt.profile(())
+            prof = opt.profile_read()
+            del opt, model
+            torch.cuda.empty_cache()
+        # timed region: plain steps, no events between the launches
+        model, opt = fresh()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            opt.step()
+        barrier()
+        elapsed = time.perf_counter() - t0
+        if dist is not None:
+            t = torch.tensor([elapsed], dtype=torch.float64, device=cdev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            elapsed = float(t.item())
+        stats = opt.last_step_stats()
+        loss = float(torch.nn.functional.mse_loss(model(x), y))
+        if dist is not None:
+            lt = torch.tensor([loss * per], dtype=torch.float64, device=cdev)
+            dist.all_reduce(lt)
+            loss = float(lt.item()) / Bg
+        del opt, model, x, y
+        torch.cuda.empty_cache()
+        return per, elapsed, prof, stats, loss
+
+    Bg = B * world if args.scaling == 'weak' else B
+    per, elapsed, prof, stats, loss = measure(Bg, True)
+    weak = None
+    if world > 1 and args.scaling == 'strong' and not args.no_weak:
+        wper, wel, _, _, _ = measure(B * world, False)
+        weak = {'global_batch': B * world, 'batch_per_gpu': wper, 'ms_per_step': round(wel / args.steps * 1e3, 4),
+                'it_s': round(args.steps / wel, 4),
+                'value': round(args.steps / wel * B * world / HEADLINE_B, 4),
+                'unit': 'batch-8192 it/s (it/s x global_batch / 8192)'}
 
     it_s = args.steps / elapsed
-    value = it_s * Bg / HEADLINE_B
+    value = it_s * Bg / HEADLINE_B if args.scaling == 'weak' else it_s
     # roofline of the dominant kernel class
     roof = None
     ranked = sorted(((ms, c) for c, (ms, n) in prof.items() if roofline_terms(c, per, T, D, H)), reverse=True)
@@ -370,8 +423,14 @@ def main():
         roof['launches'] = n
         roof = {k: (round(v, 4) if isinstance(v, float) else v) for k, v in roof.items()}
     t_roof = step_roofline_s(per, T, D, H)
-    step_roof = {'t_roof_ms': round(t_roof * 1e3, 4), 'step_frac': round(t_roof / (elapsed / args.steps), 4),
-                 'basis': 'SURVEY.md 8(d): sum over weight phase and sweep of max(F/157.3 TFLOP/s, B/8 TB/s)'}
+    t_built = step_roofline_built_s(per, T, D, H)
+    t_step = elapsed / args.steps
+    step_roof = {'t_roof_ms': round(t_roof * 1e3, 4), 'step_frac': round(t_roof / t_step, 4),
+                 'basis': 'SURVEY.md 8(d): sum over weight phase and sweep of max(F/157.3 TFLOP/s, B/8 TB/s)',
+                 't_roof_built_ms': round(t_built * 1e3, 4), 'step_frac_built': round(t_built / t_step, 4),
+                 'basis_built': 'GEMMs as built: sum over the two phases of max(sum of split-product work / '
+                                'its matrix peak (bf16/fp16 2.5 PFLOP/s: sweep 6 products, G_h 3, Q_h 2; '
+                                'x side fp32 157.3 TFLOP/s), SURVEY.md 8(d) bytes / 8 TB/s)'}
     kernel_ms = {c: {'ms_per_step': round(ms / args.steps, 4), 'launches_per_step': n / args.steps}
                  for c, (ms, n) in sorted(prof.items(), key=lambda kv: -kv[1][0])}
 
@@ -391,7 +450,17 @@ def main():
                                    f'{args.config.upper()}: ADMMBasedOptimizer.step() ({variant}), random-walk windows',
                        'global_batch': Bg, 'batch_per_gpu': per, 'seq_len': T, 'input_size': D, 'hidden': H,
                        'output_size': 1, 'params': 'GoogleStock', 'parallelism': f'dp{world}',
-                       'global_it_per_s': round(it_s, 4)},
+                       'global_it_per_s': round(it_s, 4),
+                       # the arithmetic of the step's GEMMs (all f32-accurate or trial-direction only)
+                       'gemm_arithmetic': {
+                           'sweep z = [x|h] [Wx;Wh]': 'split3 bf16, 6 products (f32-accurate)',
+                           'G_h = rho Hprev^T R': 'scaled fp16 two-way splits, 3 products (f32-accurate); '
+                                                  'split3 at the first step after (re)binding',
+                           'Q_h = Hprev G_h': 'two-piece bf16 Hprev x bf16 G, stored bf16 (line-search '
+                                              'direction only)',
+                           'x side (G_x, X G_x, X dWx)': 'fp32 MFMA',
+                           'ADMM_ATR_F16': os.environ.get('ADMM_ATR_F16', '1')}},
+            **({'weak': weak} if weak else {}),
             'roofline': roof,
             'step_roofline': step_roof,
             'cpu_baseline': cpu,

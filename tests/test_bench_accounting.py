@@ -57,3 +57,13 @@ def test_committed_bench_line_uses_survey_bytes():
     assert r['kernel'] == 'sweep' and r['algorithmic_bytes'] == bench.survey_terms(*C3)[1][1]
     assert r['frac'] == pytest.approx(r['algorithmic_bytes'] / (r['avg_launch_us'] * 1e-6) / 8e12, rel=1e-3)
     assert d['step_roofline']['step_frac'] == pytest.approx(3.768 / d['ms_per_step'], rel=1e-3)
+
+
+def test_built_roofline_basis():
+    """The second step-roofline basis prices the GEMMs at the matrix rate of the split products they
+    run as: at C3 max(0.44 ms of matrix work, 13.2 GB) + max(0.35 ms, 6.7 GB)
+    = 2.49 ms; it is below SURVEY's fp32-peak t_roof wherever the GEMMs matter (C3, C5)."""
+    assert bench.step_roofline_built_s(*C3) * 1e3 == pytest.approx(2.485, abs=0.005)
+    assert bench.step_roofline_built_s(*C5) < bench.step_roofline_s(*C5)
+    g = bench.built_gemms(*C3)
+    assert sum(f * n / p for f, n, p in g['weights']) * 1e3 == pytest.approx(0.439, abs=0.005)

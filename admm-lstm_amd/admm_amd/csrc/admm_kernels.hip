@@ -342,9 +342,13 @@ __global__ __launch_bounds__(kThreads) void k_sweep_wt16(int D, int H, int XC, W
   }
 }
 
-__global__ __launch_bounds__(kThreads) void k_sweep_wt(int D, int H, int XC, Weights w, bf16x8* __restrict__ wt) {
+__global__ __launch_bounds__(kThreads) void k_sweep_wt(int D, int H, int XC, Weights w, bf16x8* __restrict__ wt,
+                                                         unsigned* __restrict__ xcnt, int nx) {
   const int NT = H / 32, KC2 = XC + 2 * NT, XK = 16 * XC;
   const int total = 4 * NT * KC2 * 64;
+  // the column-split sweep's hand-off counters start every launch at 0 (this kernel runs right
+  // before it on the stream)
+  for (int i = blockIdx.x * kThreads + threadIdx.x; i < nx; i += gridDim.x * kThreads) xcnt[i] = 0u;
   for (int i = blockIdx.x * kThreads + threadIdx.x; i < total; i += gridDim.x * kThreads) {
     const int lane = i & 63, c = (i >> 6) % KC2, n = (i / (64 * KC2)) % NT, q = i / (64 * KC2 * NT);
     const int jj = 32 * n + (lane & 31), h = lane >> 5;
@@ -376,10 +380,23 @@ __global__ __launch_bounds__(kThreads) void k_sweep_wt(int D, int H, int XC, Wei
 // j) adds the four waves' sums of gate q, column j of that tile in wave order into a register
 // ring of the NT column tiles, and writes its slab entries at the end: a fixed summation order,
 // 8 KB of LDS and NT registers.
-template <int NT, int XC, bool GX, int ROWS = 32>
+// NC > 1 (ROWS = 32, the strong-scaling path: few rows per GPU): the column-split sweep.  Workgroup
+// (rb, cg) owns the 32 rows of row block rb and the NTC = NT / NC column tiles cg NTC .. of every t,
+// so that B = 1024 rows fill 32 x 8 = 256 CUs instead of 32.  [x_t | h_{t-1}] still lives whole in
+// each workgroup's LDS; the NC workgroups of a row block exchange h_t through memory once per t:
+// the h_t stores are write-through (sc1), every consumer wave drains them, the last of the four
+// adds to its row block's counter (agent scope), and before the producer may start the h chunks of
+// t + 1 one consumer wave polls that counter to NC t; then the consumer waves read the other
+// workgroups' columns of h_t with sc1 loads into the A image (the R1 hand-off of
+// cdna_hip_programming.md Guideline 16, with sc1 loads in place of the acquire).  The counters
+// (a.xcnt, one per row block) are zeroed by k_sweep_wt before every launch; all workgroups must be
+// resident at once (the host checks the grid against the CUs), and every spin is bounded.
+template <int NT, int XC, bool GX, int ROWS = 32, int NC = 1>
 __global__ __launch_bounds__(SR_THREADS) void k_sweep_rows(Geom g, const bf16x8* __restrict__ wt, Hyper hp,
                                                             SweepT a) {
   using SG = SrGeom<NT, XC, ROWS>;
+  static_assert(NC == 1 || (ROWS == 32 && NT % NC == 0), "column split: 32-row tiles, whole tiles per group");
+  constexpr int NTC = NT / NC;   // column tiles of this workgroup per t
   constexpr bool GXP = GX && ROWS == 32;   // G_x partials folded by the producer (MFMA)
   constexpr bool GXC = GX && ROWS == 16;   // ... accumulated by the consumer (D == 1)
   constexpr int H = SG::H, XK = SG::XK, K2 = SG::K2, KC2 = SG::KC2, AST = SG::AST, AP = SG::APIECE;
@@ -389,8 +406,18 @@ __global__ __launch_bounds__(SR_THREADS) void k_sweep_rows(Geom g, const bf16x8*
   // GXC: per step parity, consumer wave and gate, the four-row sums of the tile's TW columns
   __shared__ __attribute__((aligned(16))) float Px[GXC ? 2 : 1][GXC ? 4 : 1][GXC ? 4 : 1][GXC ? TW : 1];
   __shared__ float Rg[GXC ? 5 * 256 : 1];   // GXC: the consumer threads' running range maxima
+  // NC > 1: [0] consumer waves that have drained their h_t stores (4 per t), [1] last t whose h from
+  // the other groups of the row block may be read
+  __shared__ int xsync[2];
+  if (NC > 1 && threadIdx.x < 2) xsync[threadIdx.x] = 0;
   const int T = g.T, D = g.D;
-  const int64_t m0 = a.r0 + (int64_t)blockIdx.x * ROWS;
+  // NC > 1: block b -> (row block rb, column group cg); the NC groups of a row block are blocks
+  // b = x + 8 (NC i + cg), one XCD's under the observed round-robin placement (speed only)
+  const int rb = NC == 1 ? (int)blockIdx.x : (int)(blockIdx.x % 8) + 8 * (int)(blockIdx.x / (8 * NC));
+  const int cg = NC == 1 ? 0 : (int)((blockIdx.x / 8) % NC);
+  const int n0 = cg * NTC;        // first column tile of this workgroup
+  const int64_t m0 = a.r0 + (int64_t)rb * ROWS;
+  if (NC > 1 && m0 >= a.r1) return;   // a padding row block: its whole group exits
   const int64_t rs = (int64_t)(T + 1) * H;
   const int64_t BTH = g.BT() * H;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -472,7 +499,113 @@ __global__ __launch_bounds__(SR_THREADS) void k_sweep_rows(Geom g, const bf16x8*
     __syncthreads();         // final step: the consumer drains the last tile
     return;
   }
-  if (ROWS == 32 && wave < 4) {
+  if (NC > 1 && wave < 4) {
+    // ------------------------------------------------------------------ producer, column split
+    // As the row producer below over this group's NTC tiles only, the chunk sequence flattened
+    // over t with a U-deep ring (GTC = NTC KC2 chunks per t need not divide by U).  The mid-step
+    // barrier comes before the first h chunk of every t (h_{t-1} of the other groups arrives then);
+    // the end-of-step barrier right at each tile's end, and the G_x fold (GX) after it.
+    constexpr int U = 4, GTC = NTC * KC2;
+    static_assert(GTC >= U, "ring deeper than the chunk cycle");
+    const int q = wave, c = lane & 31, kh = lane >> 5;
+    const bf16x8* wq = wt + ((size_t)q * SG::GT + (size_t)n0 * KC2) * 3 * 64 + lane;   // [q][n][c]: contiguous
+    bf16x8 bq[U][3];
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int p = 0; p < 3; ++p) bq[u][p] = wq[(u * 3 + p) * 64];
+    f32x16 acc = {};
+    f32x4 gx[NTC][2];
+    float xcur[8], xnext[8];
+    int gxs = 0;
+    auto load_gx_x = [&](int tn, float (&xv)[8]) {
+#pragma unroll
+      for (int ks = 0; ks < 8; ++ks) {
+        const int64_t b = min(m0 + 4 * ks + (lane >> 4), a.r1 - 1);
+        const int d = lane & 15;
+        xv[ks] = d < D ? a.x[(b * T + (tn - 1)) * D + d] : 0.f;
+      }
+    };
+    auto gx_fold = [&](int buf) {
+      if ((gxs % NTC) == 0) {
+#pragma unroll
+        for (int ks = 0; ks < 8; ++ks) xcur[ks] = xnext[ks];
+        const int tn = gxs / NTC + 2;
+        if (tn <= T) load_gx_x(tn, xnext);
+      }
+      const float* Rq = &Zb[buf][q * ZG + (lane >> 4) * 32 + (lane & 15)];
+#pragma unroll
+      for (int ks = 0; ks < 8; ++ks)
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+          gx[0][h] = __builtin_amdgcn_mfma_f32_16x16x4f32(xcur[ks], Rq[4 * ks * 32 + 16 * h], gx[0][h], 0, 0, 0);
+      const f32x4 r0 = gx[0][0], r1 = gx[0][1];
+#pragma unroll
+      for (int k = 0; k + 1 < NTC; ++k) {
+        gx[k][0] = gx[k + 1][0];
+        gx[k][1] = gx[k + 1][1];
+      }
+      gx[NTC - 1][0] = r0;
+      gx[NTC - 1][1] = r1;
+      ++gxs;
+    };
+    if constexpr (GX) {
+#pragma unroll
+      for (int k = 0; k < NTC; ++k) gx[k][0] = gx[k][1] = f32x4{};
+      load_gx_x(1, xnext);
+    }
+    const int total = T * GTC;
+#pragma unroll 1
+    for (int G0 = 0; G0 < total; G0 += U) {
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int G = G0 + u;
+        if (G < total) {
+          const int t = G / GTC + 1, r = G - (t - 1) * GTC, nl = r / KC2, cc = r - nl * KC2;
+          if (nl == 0 && cc == XC) SR_SYNC();   // mid-step: all of h_{t-1} is in this A buffer
+          const __bf16* A = &Ab[t & 1][c * AST + 8 * kh];
+          const bf16x8 a0 = *reinterpret_cast<const bf16x8*>(A + 16 * cc);
+          const bf16x8 a1 = *reinterpret_cast<const bf16x8*>(A + AP + 16 * cc);
+          const bf16x8 a2 = *reinterpret_cast<const bf16x8*>(A + 2 * AP + 16 * cc);
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a2, bq[u][0], acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, bq[u][1], acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, bq[u][2], acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, bq[u][0], acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, bq[u][1], acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, bq[u][0], acc, 0, 0, 0);
+          const int rn = r + U < GTC ? r + U : r + U - GTC;
+#pragma unroll
+          for (int p = 0; p < 3; ++p) bq[u][p] = wq[(rn * 3 + p) * 64];
+          if (cc == KC2 - 1) {
+            const int st = (t - 1) * NTC + nl;   // step index
+            float* Z = &Zb[st & 1][q * ZG + c];
+#pragma unroll
+            for (int rr = 0; rr < 16; ++rr) Z[acc_row(rr, lane) * 32] = acc[rr];
+            acc = f32x16{};
+            SR_SYNC();   // end of step
+            if constexpr (GX)
+              if (st >= 1) gx_fold((st - 1) & 1);
+          }
+        }
+      }
+    }
+    __syncthreads();         // final step: the consumer drains the last tile
+    if constexpr (GX) {
+      gx_fold((T * NTC - 1) & 1);
+      float* out = a.gx_slab + ((int64_t)rb * 4 + q) * D * H;
+#pragma unroll
+      for (int k = 0; k < NTC; ++k)
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+          for (int v = 0; v < 4; ++v) {
+            const int d = 4 * (lane >> 4) + v;
+            if (d < D) out[(int64_t)d * H + 32 * (n0 + k) + 16 * h + (lane & 15)] = gx[k][h][v];
+          }
+    }
+    return;
+  }
+  if (ROWS == 32 && NC == 1 && wave < 4) {
     // ------------------------------------------------------------------ producer (gate q)
     // The B stream of a wave is the cyclic sequence of its GT chunks per t (3 x 16 B per lane
     // each).  The loop walks it U chunks at a time with a U-deep register ring: slot u holds
@@ -642,12 +775,55 @@ __global__ __launch_bounds__(SR_THREADS) void k_sweep_rows(Geom g, const bf16x8*
     }
   };
 
+  // NC > 1: publish this group's h_t (sc1 stores, drained by every consumer wave, the last of the
+  // four adds to the row block's counter), wait until the NC groups have published, then read the
+  // other groups' columns of h_t with sc1 loads into the A image of t + 1 (split3, as put_a).
+  auto exchange = [&](int t) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's h_t stores have completed
+    if (lane == 0) {
+      const int old = atomicAdd(&xsync[0], 1);
+      if (old == 4 * t - 1) __hip_atomic_fetch_add(a.xcnt + rb, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (ct < 64) {   // one wave polls the counter (relaxed, agent scope: an sc1 load), bounded
+      const unsigned want = (unsigned)(NC * t);
+      for (unsigned spins = 0; __hip_atomic_load(a.xcnt + rb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < want;) {
+        if (++spins > (1u << 24)) {   // ~0.5 s: a group never arrived (not resident?) -- give up, flagged
+          if (lane == 0 && a.fail) atomicAdd(a.fail, 1);
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+      if (lane == 0) __hip_atomic_store(&xsync[1], t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+    while (__hip_atomic_load(&xsync[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < t) __builtin_amdgcn_s_sleep(1);
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // keep the loads below the poll
+    constexpr int C4 = H / 4, NL = ROWS * C4 / 256;           // float4 of h_t per thread
+    f32x4 hv[NL];
+#pragma unroll
+    for (int i = 0; i < NL; ++i) {
+      const int f = ct + 256 * i, hr = f / C4, col = 4 * (f % C4);
+      const bool own = col >= TW * n0 && col < TW * (n0 + NTC);
+      const uint32_t off = (uint32_t)(((m0 + hr) * rs + (int64_t)t * H + col) * 4);
+      hv[i] = own ? f32x4{} : buf_ld4<kAuxL2>(rS[5], off);   // rows past r1 read 0
+    }
+#pragma unroll
+    for (int i = 0; i < NL; ++i) {
+      const int f = ct + 256 * i, hr = f / C4, col = 4 * (f % C4);
+      if (col >= TW * n0 && col < TW * (n0 + NTC)) continue;
+      bf16x4 p0, p1, p2;
+      split3(hv[i], p0, p1, p2);
+      __bf16* d = &Ab[(t + 1) & 1][hr * AST + XK + col];
+      *reinterpret_cast<bf16x4*>(d) = p0;
+      *reinterpret_cast<bf16x4*>(d + AP) = p1;
+      *reinterpret_cast<bf16x4*>(d + 2 * AP) = p2;
+    }
+  };
   // Tile operands are loaded one tile early (loading two tiles ahead measured no faster).
   // cring[0] is c_{t-1} of the tile being updated: popped at every tile, c_t pushed at the back.
   static_assert(NT > 1, "the mid-step barrier protocol needs two or more column tiles");
-  f32x4 cring[NT];
+  f32x4 cring[NTC];
 #pragma unroll
-  for (int k = 0; k < NT; ++k) cring[k] = f32x4{};
+  for (int k = 0; k < NTC; ++k) cring[k] = f32x4{};
   // GXC: this thread's slab entries (gate = its consumer wave, column = its lane) of each column
   // tile, a ring turned once per step like cring
   float gxr[GXC ? NT : 1];   // slot 0 = the tile summed next (turned once per step)
@@ -666,7 +842,7 @@ __global__ __launch_bounds__(SR_THREADS) void k_sweep_rows(Geom g, const bf16x8*
     for (int k = 0; k < 5; ++k) Rg[k * 256 + ct] = 0.f;
   }
   St4 nxt;
-  load_tile(1, 0, nxt);
+  load_tile(1, n0, nxt);
   load_x(2);                 // step 0: the producer computes tile (1, 0)
   __syncthreads();           // its mid-step barrier
   __syncthreads();           // end of step 0
@@ -674,7 +850,8 @@ __global__ __launch_bounds__(SR_THREADS) void k_sweep_rows(Geom g, const bf16x8*
     const bool last = (t == T);
     __bf16* An = &Ab[(t + 1) & 1][row * AST + XK + j4];
 #pragma unroll 1
-    for (int n = 0; n < NT; ++n) {
+    for (int nl = 0; nl < NTC; ++nl) {
+      const int n = n0 + nl;   // column tile (NC == 1: n0 = 0)
 #ifdef SR_TIMING
       const unsigned long long ta_ = clock64();
 #endif
@@ -686,9 +863,9 @@ __global__ __launch_bounds__(SR_THREADS) void k_sweep_rows(Geom g, const bf16x8*
       const unsigned long long tw_ = clock64();
       if ((threadIdx.x & 63) == 0) sr_lw += tw_ - ta_;
 #endif
-      if (n + 1 < NT) load_tile(t, n + 1, nxt);
-      else if (!last) load_tile(t + 1, 0, nxt);
-      f32x4* Z = reinterpret_cast<f32x4*>(&Zb[((t - 1) * NT + n) & 1][row * TW + j4]);
+      if (nl + 1 < NTC) load_tile(t, n + 1, nxt);
+      else if (!last) load_tile(t + 1, n0, nxt);
+      f32x4* Z = reinterpret_cast<f32x4*>(&Zb[((t - 1) * NTC + nl) & 1][row * TW + j4]);
       constexpr int ZG4 = ZG / 4;   // one gate's tile in f32x4
       const f32x4 zi = Z[0], zf = Z[ZG4], zg = Z[2 * ZG4], zo = Z[3 * ZG4];
       f32x4 i1, f1, g1, o1, c1, h1, li, lf, lg, lo, lc;
@@ -707,8 +884,8 @@ __global__ __launch_bounds__(SR_THREADS) void k_sweep_rows(Geom g, const bf16x8*
         di[u] = o.di; df[u] = o.df; dg[u] = o.dg; dO[u] = o.dO;
       }
 #pragma unroll
-      for (int k = 0; k + 1 < NT; ++k) cring[k] = cring[k + 1];
-      cring[NT - 1] = c1;
+      for (int k = 0; k + 1 < NTC; ++k) cring[k] = cring[k + 1];
+      cring[NTC - 1] = c1;
       // lam/rho + S of the updated i, f, g, o: the next x stage's targets (tgt_quot, as k_resid_gx)
       f32x4 ti, tf, tg, to;
       if (hp.rinv_exact) {   // workgroup-uniform: 16 IEEE divisions per tile and thread saved
@@ -788,7 +965,7 @@ __global__ __launch_bounds__(SR_THREADS) void k_sweep_rows(Geom g, const bf16x8*
       const uint32_t po = pofs + (uint32_t)(t * H + TW * n) * 4, zo4 = zofs + (uint32_t)((t - 1) * H + TW * n) * 4;
       buf_st4(rS[0], po, i1); buf_st4(rS[1], po, f1); buf_st4(rS[2], po, g1); buf_st4(rS[3], po, o1);
       buf_st4<0>(rS[4], po, c1);             // c_t: read by the next step's kernels
-      if (!last) buf_st4<0>(rS[5], po, h1);
+      if (!last) buf_st4<NC == 1 ? 0 : 16>(rS[5], po, h1);   // NC > 1: write-through (sc1), handed off
       buf_st4(rL[0], po, li); buf_st4(rL[1], po, lf); buf_st4(rL[2], po, lg); buf_st4(rL[3], po, lo);
       buf_st4(rL[4], po, lc);
       // one descriptor spans the 4 planes, so its record count cannot drop the stores of rows
@@ -805,8 +982,9 @@ __global__ __launch_bounds__(SR_THREADS) void k_sweep_rows(Geom g, const bf16x8*
       const unsigned long long tc_ = clock64();
       if ((threadIdx.x & 63) == 0) { sr_comp += tb_ - ta_; sr_store += tc_ - tb_; }
 #endif
-      if (n == NT - 1 && !last) {
-        load_x(t + 2);       // the producer's next tile is (t+1, 0)
+      if (nl == NTC - 1 && !last) {
+        load_x(t + 2);       // the producer's next tile is (t+1, n0)
+        if constexpr (NC > 1) exchange(t);   // the other groups' columns of h_t into this A buffer
         SR_SYNC();           // its mid-step barrier: h_t is complete
       }
       SR_SYNC();             // end of step
@@ -2963,6 +3141,20 @@ bool sweep_rows_ok(const Geom& g) {
 bool sweep_rows_gx_ok(const Geom& g) { return sweep_rows_ok(g) && (sweep_r16(g) ? g.D == 1 : g.D <= 16); }
 int sweep_rows_blocks(const Geom& g) { return (int)((g.B + (sweep_r16(g) ? 15 : 31)) / (sweep_r16(g) ? 16 : 32)); }
 
+// Column groups of the persistent sweep (k_sweep_rows NC): 1 while the 32-row blocks alone give a
+// workgroup to at least half of the 256 CUs; else the largest of 8, 4, 2 whose padded grid
+// (row blocks rounded up to 8, times the groups) still has one workgroup per CU.  H = 256 only.
+int sweep_rows_nc(const Geom& g) {
+  if (sweep_r16(g) || g.H != 256 || !sweep_rows_ok(g)) return 1;
+  const int64_t nrb = (g.B + 31) / 32, pad = (nrb + 7) / 8 * 8;
+  if (nrb >= 128) return 1;
+  for (int nc : {8, 4, 2})
+    if (pad * nc <= kSweepCUs) return nc;
+  return 1;
+}
+
+int sweep_xcnt_words(const Geom& g) { return (int)(((g.B + 31) / 32 + 7) / 8 * 8); }
+
 static int sweep_xc(const Geom& g) { return sweep_r16(g) ? (g.D + 31) / 32 : (g.D + 15) / 16; }
 
 size_t sweep_wt_floats(const Geom& g) {   // bf16x8 image, in float units
@@ -2970,7 +3162,7 @@ size_t sweep_wt_floats(const Geom& g) {   // bf16x8 image, in float units
   return (size_t)4 * (g.H / 32) * (sweep_xc(g) + 2 * (g.H / 32)) * 3 * 64 * 4;
 }
 
-void launch_sweep_wt(const Geom& g, const Weights& w, float* wt, hipStream_t s) {
+void launch_sweep_wt(const Geom& g, const Weights& w, float* wt, hipStream_t s, unsigned* xcnt) {
   const int xc = sweep_xc(g);
   if (sweep_r16(g)) {
     const int total = 4 * (g.H / 64) * (xc + g.H / 32) * 4 * 64;
@@ -2979,7 +3171,8 @@ void launch_sweep_wt(const Geom& g, const Weights& w, float* wt, hipStream_t s) 
   }
   const int NT = g.H / 32;
   const int total = 4 * NT * (xc + 2 * NT) * 64;
-  k_sweep_wt<<<cdiv64(total, kThreads), kThreads, 0, s>>>(g.D, g.H, xc, w, reinterpret_cast<bf16x8*>(wt));
+  k_sweep_wt<<<cdiv64(total, kThreads), kThreads, 0, s>>>(g.D, g.H, xc, w, reinterpret_cast<bf16x8*>(wt), xcnt,
+                                                         xcnt ? sweep_xcnt_words(g) : 0);
 }
 
 template <int XC>
@@ -2995,6 +3188,19 @@ static void launch_sweep_rows_xc(const Geom& g, const bf16x8* wt, const Hyper& h
 #undef SR16_CASE
       default: break;
     }
+    return;
+  }
+  const int nc = a.xcnt ? sweep_rows_nc(g) : 1;
+  if (nc > 1 && g.H == 256) {   // column split (strong-scaling ranks): padded row blocks x nc groups
+    dim3 grid((unsigned)(sweep_xcnt_words(g) * nc));
+    auto go = [&](auto ncv) {
+      constexpr int NCV = decltype(ncv)::value;
+      if (XC == 1 && a.gx_slab) k_sweep_rows<8, XC, true, 32, NCV><<<grid, SR_THREADS, 0, s>>>(g, wt, hp, a);
+      else k_sweep_rows<8, XC, false, 32, NCV><<<grid, SR_THREADS, 0, s>>>(g, wt, hp, a);
+    };
+    if (nc == 8) go(std::integral_constant<int, 8>{});
+    else if (nc == 4) go(std::integral_constant<int, 4>{});
+    else go(std::integral_constant<int, 2>{});
     return;
   }
   dim3 grid(cdiv64(a.r1 - a.r0, SR_ROWS));

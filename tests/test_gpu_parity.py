@@ -907,6 +907,45 @@ def test_atr_fp16_split_matches_split3(shape, mods, dev, monkeypatch):
     assert out[1][3] == pytest.approx(out[0][3], rel=1e-5)
 
 
+@pytest.mark.parametrize('B', [1024, 2048, 1000, 300])
+def test_column_split_sweep_bit_identical(B, mods, dev, monkeypatch):
+    """The column-split persistent sweep (k_sweep_rows NC > 1: a strong-scaling rank's few rows over
+    8, 4 or 2 column groups per row block, h_t handed between the groups through memory once per t)
+    against the row-block sweep (ADMM_SWEEP_SPLIT_COLS=0): the same products in the same order, so
+    weights, exponents, gates, duals and the z cache are bitwise equal over four steps (with the
+    next x stage's G_x partials from the sweep).  B = 1000 and 300: padded row blocks."""
+    from blocks.lstm import LSTM
+    from parameters import example_parameter_dictionary
+    from admm_amd import _native as N
+    admm, _ = mods
+    admm.with_dual_y = False
+    T, D, H = 6, 16, 256
+    g = torch.Generator().manual_seed(41)
+    x = torch.rand(B, T, D, generator=g).to(dev)
+    y = (0.8 * x.mean((1, 2)).unsqueeze(1) + 0.1 * torch.rand(B, 1, generator=g).to(dev)).contiguous()
+    out = []
+    for mode in ('0', '1'):
+        monkeypatch.setenv('ADMM_SWEEP_SPLIT_COLS', mode)
+        torch.manual_seed(0)
+        m = LSTM(D, H, 1).to(dev)
+        opt = admm.ADMMBasedOptimizer(m, (x, y), example_parameter_dictionary['GoogleStock'], verbose=False)
+        ks = []
+        for _ in range(4):
+            opt.step()
+            st = opt.last_step_stats()
+            assert st['nonfinite'] == 0 and st['unresolved'] == 0, st
+            ks.append(list(st['k'].values()))
+        zc = torch.empty(4, B * T, H, device=dev)
+        assert N.load().admm_debug_workspace(opt._ctx, 0, N.ptr(zc), zc.numel() * 4, N.stream_handle(dev)) == 1
+        out.append((ks, torch.cat([p.detach().flatten() for p in m.parameters()]
+                                  + [v.flatten() for v in opt.gates.values()]
+                                  + [v.flatten() for v in opt.duals.values()]), zc))
+        del opt
+    assert out[0][0] == out[1][0]
+    assert torch.equal(out[0][1], out[1][1])
+    assert torch.equal(out[0][2], out[1][2])
+
+
 def test_generic_weight_stage_matches_fast(mods, dev, monkeypatch):
     """ADMM_GENERIC=1 runs the weight stages on the generic kernels (materialised R and Q, f32 MFMA
     GEMMs) instead of the fast streaming path.  Step 1 decides identically on both: the x-side

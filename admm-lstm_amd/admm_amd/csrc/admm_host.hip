@@ -77,6 +77,13 @@ int dalloc(T** p, size_t n) {
 }  // namespace
 
 constexpr int kMaxSweepStreams = 4;
+
+struct StepSig {   // admm_step's launch-sequence signature (see step_sig)
+  uint32_t flags;
+  AdmmBuffers buf;
+  float* trace[4];
+  void* comm;
+};
 constexpr int kMaxOutputs = 4096;
 
 struct AdmmCtx {
@@ -165,6 +172,14 @@ struct AdmmCtx {
   // admm_debug_force: forced line-search decisions [8 exponents, h_T failing tests] (tests)
   int* force_dev = nullptr;
   bool force_on = false;
+  // steady-state step graph (ADMM_GRAPH=1, admm_step)
+  bool graph = false;
+  hipStream_t gs = nullptr;
+  hipEvent_t ev_gfork = nullptr, ev_gjoin = nullptr;
+  hipGraphExec_t gexec = nullptr;
+  StepSig gsig{}, last_sig{};
+  bool have_last_sig = false;
+  int64_t graph_replays = 0;
 };
 
 namespace {
@@ -533,6 +548,7 @@ int admm_create(const AdmmDims* dims, const AdmmParams* params, int device, Admm
   if (const char* e = std::getenv("ADMM_SPLIT3")) c->split3 = c->split3 && std::atoi(e) != 0;
   if (const char* e = std::getenv("ADMM_P16")) c->p16 = std::atoi(e) != 0;
   if (const char* e = std::getenv("ADMM_ATR_F16")) c->atr_f16 = std::atoi(e) != 0;
+  if (const char* e = std::getenv("ADMM_GRAPH")) c->graph = std::atoi(e) != 0;
   Hyper& h = c->hp;
   for (int i = 0; i < 7; ++i) h.rho[i] = params->rho[i];
   h.rinv_exact = 1;
@@ -591,7 +607,10 @@ int admm_create(const AdmmDims* dims, const AdmmParams* params, int device, Admm
     admm_destroy(c);
     return fail(rc, "%s", msg.c_str());
   }
-  bool ok = hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) == hipSuccess;
+  bool ok = hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) == hipSuccess &&
+            hipEventCreateWithFlags(&c->ev_gfork, hipEventDisableTiming) == hipSuccess &&
+            hipEventCreateWithFlags(&c->ev_gjoin, hipEventDisableTiming) == hipSuccess &&
+            hipStreamCreateWithFlags(&c->gs, hipStreamNonBlocking) == hipSuccess;
   for (int p = 0; ok && p < kMaxSweepStreams - 1; ++p)
     ok = hipStreamCreateWithFlags(&c->sx[p], hipStreamNonBlocking) == hipSuccess &&
          hipEventCreateWithFlags(&c->ev_join[p], hipEventDisableTiming) == hipSuccess;
@@ -624,6 +643,10 @@ int admm_destroy(AdmmCtx* c) {
   if (c->status_host) (void)hipHostFree(c->status_host);
   for (hipEvent_t e : c->ev_pool) (void)hipEventDestroy(e);
   if (c->ev_fork) (void)hipEventDestroy(c->ev_fork);
+  if (c->gexec) (void)hipGraphExecDestroy(c->gexec);
+  if (c->ev_gfork) (void)hipEventDestroy(c->ev_gfork);
+  if (c->ev_gjoin) (void)hipEventDestroy(c->ev_gjoin);
+  if (c->gs) (void)hipStreamDestroy(c->gs);
   for (int p = 0; p < kMaxSweepStreams - 1; ++p) {
     if (c->ev_join[p]) (void)hipEventDestroy(c->ev_join[p]);
     if (c->sx[p]) (void)hipStreamDestroy(c->sx[p]);
@@ -712,11 +735,24 @@ int admm_init_state(AdmmCtx* c, void* stream) {
   return ADMM_OK;
 }
 
-int admm_step(AdmmCtx* c, void* stream) {
-  if (!c) return fail(ADMM_EINVAL, "NULL ctx");
-  if (!c->bound) return fail(ADMM_ESTATE, "admm_step before admm_bind");
-  hipStream_t s = (hipStream_t)stream;
-  DEVICE_GUARD(c->device);
+namespace {
+
+// Everything the launch sequence of one step depends on besides the device data: two steps with
+// equal signatures enqueue the same kernels with the same arguments (the steady state).
+StepSig step_sig(const AdmmCtx* c) {
+  StepSig g{};
+  g.flags = (c->z_valid ? 1u : 0u) | (c->tgt_valid ? 2u : 0u) | (c->gx_valid ? 4u : 0u) | (c->range_valid ? 8u : 0u) |
+            (c->x1_valid ? 16u : 0u) | (c->lamh_known ? 32u : 0u) | (c->hp.with_dual_y ? 64u : 0u) |
+            (c->force_on ? 128u : 0u) | (c->prof_mask ? 256u : 0u) | (c->host_ar ? 512u : 0u);
+  g.buf = c->buf;
+  g.trace[0] = c->trace_g[0]; g.trace[1] = c->trace_g[1]; g.trace[2] = c->trace_r[0]; g.trace[3] = c->trace_r[1];
+  g.comm = c->comm;
+  return g;
+}
+
+bool sig_eq(const StepSig& a, const StepSig& b) { return std::memcmp(&a, &b, sizeof a) == 0; }
+
+int run_step(AdmmCtx* c, hipStream_t s) {
   int rc;
   if (!c->z_valid) {
     ProfScope ps(c, ADMM_PROF_ZGEMM, s);
@@ -731,6 +767,68 @@ int admm_step(AdmmCtx* c, void* stream) {
   c->tgt_valid = c->sweep_rows && fast_path(c->g) && c->tgt_sweep;
   c->gx_valid = c->tgt_valid && c->gx_slab != nullptr;
   c->range_valid = c->sweep_rows;   // the persistent sweep tracked the next weight phase's operand ranges
+  return ADMM_OK;
+}
+
+void drop_graph(AdmmCtx* c) {
+  if (c->gexec) (void)hipGraphExecDestroy(c->gexec);
+  c->gexec = nullptr;
+}
+
+}  // namespace
+
+// Steady-state steps replay one HIP graph (ADMM_GRAPH=1): once two consecutive steps start from the
+// same signature (step_sig), the next one is captured on the context's own stream (the caller's may
+// be the legacy default stream, which cannot be captured), instantiated, and replayed from then on
+// while the signature holds, forked from and joined back to the caller's stream by events.  Any
+// change (re-binding, invalidation, profiling, a debug hook, with_dual_y) runs the step eagerly.
+// The host-staged communicator synchronises inside the step and is never captured.
+int admm_step(AdmmCtx* c, void* stream) {
+  if (!c) return fail(ADMM_EINVAL, "NULL ctx");
+  if (!c->bound) return fail(ADMM_ESTATE, "admm_step before admm_bind");
+  hipStream_t s = (hipStream_t)stream;
+  DEVICE_GUARD(c->device);
+  int rc;
+  const StepSig sig = step_sig(c);
+  const bool capturable = c->graph && !c->prof_mask && !c->host_ar;
+  if (capturable && c->gexec && sig_eq(sig, c->gsig)) {
+    HIP_TRY(hipEventRecord(c->ev_gfork, s));
+    HIP_TRY(hipStreamWaitEvent(c->gs, c->ev_gfork, 0));
+    HIP_TRY(hipGraphLaunch(c->gexec, c->gs));
+    HIP_TRY(hipEventRecord(c->ev_gjoin, c->gs));
+    HIP_TRY(hipStreamWaitEvent(s, c->ev_gjoin, 0));
+    c->steps++;
+    c->graph_replays++;
+    return ADMM_OK;
+  }
+  if (capturable && c->have_last_sig && sig_eq(sig, c->last_sig)) {
+    drop_graph(c);
+    hipGraph_t graph = nullptr;
+    HIP_TRY(hipEventRecord(c->ev_gfork, s));
+    HIP_TRY(hipStreamWaitEvent(c->gs, c->ev_gfork, 0));
+    HIP_TRY(hipStreamBeginCapture(c->gs, hipStreamCaptureModeRelaxed));
+    rc = run_step(c, c->gs);
+    hipError_t e = hipStreamEndCapture(c->gs, &graph);
+    if (rc) {
+      if (graph) (void)hipGraphDestroy(graph);
+      return rc;
+    }
+    if (e == hipSuccess) e = hipGraphInstantiate(&c->gexec, graph, nullptr, nullptr, 0);
+    if (graph) (void)hipGraphDestroy(graph);
+    if (e != hipSuccess) {
+      c->gexec = nullptr;
+      return fail(ADMM_EHIP, "step graph capture failed: %s", hipGetErrorString(e));
+    }
+    c->gsig = step_sig(c);   // == sig: the steady step leaves the flags as it found them
+    HIP_TRY(hipGraphLaunch(c->gexec, c->gs));
+    HIP_TRY(hipEventRecord(c->ev_gjoin, c->gs));
+    HIP_TRY(hipStreamWaitEvent(s, c->ev_gjoin, 0));
+    c->steps++;
+    return ADMM_OK;
+  }
+  if ((rc = run_step(c, s))) return rc;
+  c->last_sig = sig;
+  c->have_last_sig = true;
   c->steps++;
   return ADMM_OK;
 }

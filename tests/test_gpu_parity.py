@@ -946,6 +946,40 @@ def test_column_split_sweep_bit_identical(B, mods, dev, monkeypatch):
     assert torch.equal(out[0][2], out[1][2])
 
 
+@pytest.mark.parametrize('shape', [(2048, 8, 16, 256), (1024, 4, 16, 256), (300, 3, 16, 64)])
+def test_step_graph_bit_identical(shape, mods, dev, monkeypatch):
+    """ADMM_GRAPH=1: once two steps start from the same launch signature, the step is captured into
+    one HIP graph and replayed.  Seven steps with an external weight write after step 4 (the caches
+    are invalidated: eager steps, then a new capture) are bitwise equal to the eager run."""
+    from blocks.lstm import LSTM
+    from parameters import example_parameter_dictionary
+    admm, _ = mods
+    admm.with_dual_y = False
+    B, T, D, H = shape
+    g = torch.Generator().manual_seed(43)
+    x = torch.rand(B, T, D, generator=g).to(dev)
+    y = (0.8 * x.mean((1, 2)).unsqueeze(1) + 0.1 * torch.rand(B, 1, generator=g).to(dev)).contiguous()
+    out = []
+    for mode in ('0', '1'):
+        monkeypatch.setenv('ADMM_GRAPH', mode)
+        torch.manual_seed(0)
+        m = LSTM(D, H, 1).to(dev)
+        opt = admm.ADMMBasedOptimizer(m, (x, y), example_parameter_dictionary['GoogleStock'], verbose=False)
+        ks = []
+        for s_ in range(7):
+            opt.step()
+            ks.append(list(opt.last_step_stats()['k'].values()))
+            if s_ == 3:
+                with torch.no_grad():
+                    m.out.mul_(1.0001)
+        out.append((ks, torch.cat([p.detach().flatten() for p in m.parameters()]
+                                  + [v.flatten() for v in opt.gates.values()]
+                                  + [v.flatten() for v in opt.duals.values()])))
+        del opt
+    assert out[0][0] == out[1][0]
+    assert torch.equal(out[0][1], out[1][1])
+
+
 def test_generic_weight_stage_matches_fast(mods, dev, monkeypatch):
     """ADMM_GENERIC=1 runs the weight stages on the generic kernels (materialised R and Q, f32 MFMA
     GEMMs) instead of the fast streaming path.  Step 1 decides identically on both: the x-side

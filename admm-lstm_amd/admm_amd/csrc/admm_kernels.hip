@@ -2889,7 +2889,8 @@ __device__ __forceinline__ float ht_grad(const Geom& g, const Hyper& hp, const H
 // OC > 0: compile-time output count; OC == 0: runtime g.O, 4 * g.O floats of dynamic LDS
 template <int OC>
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(8))) void k_ht_partial(Geom g, Hyper hp, Planes6 S, Planes6 L, const float* a,
-                                                           const float* Ly, const float* wy, double* part) {
+                                                           const float* Ly, const float* wy, double* part,
+                                                           bool gcache) {
   constexpr int CW = OC > 0 ? OC : kOChunk;
   const int NO = OC > 0 ? OC : g.O;
   extern __shared__ float ht_u[];
@@ -2917,13 +2918,18 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(8))) v
     for (int o = 0; o < NO; ++o) fh += r.get(o) * r.get(o);
     float ip[kHTCand], nq[kHTCand], fb[kHTCand];
     for (int c = 0; c < kHTCand; ++c) ip[c] = nq[c] = fb[c] = 0.f;
+    // runtime O (several output chunks): the gradient g_j, an O-long dot product per j, is formed
+    // once per row into the wave's LDS row (gcache) instead of once per chunk
+    float* gc = OC == 0 && gcache ? ht_u + 4 * NO + w * g.H : nullptr;
+    if (gc)
+      for (int j = lane; j < g.H; j += kWave) gc[j] = ht_grad<OC>(g, hp, r, wy, j);
     for (int o0 = 0; o0 < NO; o0 += CW) {
       const int nw = NO - o0 < CW ? NO - o0 : CW;
       float v[kHTCand][CW];
       for (int c = 0; c < kHTCand; ++c)
         for (int oo = 0; oo < CW; ++oo) v[c][oo] = 0.f;
       for (int j = lane; j < g.H; j += kWave) {
-        const float gj = ht_grad<OC>(g, hp, r, wy, j);
+        const float gj = gc ? gc[j] : ht_grad<OC>(g, hp, r, wy, j);   // (each lane reads its own j)
         const float hj = h[j], pj = rh * o_[j] * tanhf(c_[j]) - lh[j];
         for (int c = 0; c < kHTCand; ++c) {
           const float th = ldexpf(0.1f, c);
@@ -3501,8 +3507,14 @@ int ht_blocks(const Geom& g) {   // one row per wave up to B = 8192 (each row is
 
 void launch_ht_partial(const Geom& g, const Hyper& hp, const Planes6& S, const Planes6& L, const float* a,
                        const float* Ly, const float* wy, double* part, int nblk, hipStream_t s) {
-  if (g.O == 1) k_ht_partial<1><<<nblk, kThreads, 0, s>>>(g, hp, S, L, a, Ly, wy, part);
-  else k_ht_partial<0><<<nblk, kThreads, 4 * g.O * sizeof(float), s>>>(g, hp, S, L, a, Ly, wy, part);
+  if (g.O == 1) {
+    k_ht_partial<1><<<nblk, kThreads, 0, s>>>(g, hp, S, L, a, Ly, wy, part, false);
+    return;
+  }
+  // more than one output chunk: cache g_j per wave in LDS while that fits 64 KB
+  const size_t lds = 4 * (size_t)g.O * sizeof(float), lds_g = lds + 4 * (size_t)g.H * sizeof(float);
+  const bool gc = g.O > kOChunk && lds_g <= 64 * 1024;
+  k_ht_partial<0><<<nblk, kThreads, gc ? lds_g : lds, s>>>(g, hp, S, L, a, Ly, wy, part, gc);
 }
 
 void launch_ht_reduce(const double* part, int nblk, double* sums, hipStream_t s) {

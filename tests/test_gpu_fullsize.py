@@ -59,29 +59,44 @@ def _full_fp64(g, W, S, L, dev):
     return [(k, m) for _, k, m in dec['weights']], dec['grads']
 
 
+def _pre_targets(g, opt, dev):
+    """The pre-step targets dual/rho + gate of the four gates (admm.py:308-309, fp32) and H_prev,
+    [B*T, H] each -- a fifth of cloning every gate and dual plane."""
+    B, T, H = g.B, g.T, g.H
+    tg = [(opt.duals[q][:, 1:, :] / opt.rhos[q].to(dev) + opt.gates[q][:, 1:, :]).reshape(B * T, H) for q in 'ifgo']
+    return tg, opt.gates['h'][:, :T, :].reshape(B * T, H).clone()
+
+
 def _same_input_fp64(g, opt, pre, gx, gh, model, dev):
     """fp64 search of every gate weight from the library's own inputs: its z cache and targets
     before the step, the G of each stage (admm_debug_trace), the x side's update for the h side's
-    z (admm.py:298-300: the h search sees the new x2q)."""
+    z (admm.py:298-300: the h search sees the new x2q).  pre = (zc, W0, S, L) or
+    (zc, W0, (targets, H_prev)) from _pre_targets."""
     B, T, D, H = g.B, g.T, g.D, g.H
-    zc, W0, S, L = pre
+    zc, W0 = pre[0], pre[1]
+    if len(pre) == 3:
+        tgts, Hp = pre[2]
+    else:
+        S, L = pre[2], pre[3]
+        tgts = [(L[q][:, 1:, :] / opt.rhos[q].to(dev) + S[q][:, 1:, :]).reshape(B * T, H) for q in 'ifgo']
+        Hp = S['h'][:, :T, :].reshape(B * T, H)
     X = g.x.to(dev).reshape(B * T, D)
-    Hp = S['h'][:, :T, :].reshape(B * T, H)
     out = []
     for qi, q in enumerate('ifgo'):
         rho = float(opt.rhos[q])
-        tgt = (L[q][:, 1:, :] / opt.rhos[q].to(dev) + S[q][:, 1:, :]).reshape(B * T, H)   # admm.py:308-309, fp32
+        tgt = tgts[qi]
         out.append(O.fp64_search(q, zc[qi], tgt, X, gx[qi], rho, T, orig=True))
         dwx = getattr(model, f'x2{q}').detach().double() - W0[f'x2{q}'].double()
         zh = (zc[qi].double() + X.double() @ dwx).float()   # the h stage's z, fp32 as the library holds it
         out.append(O.fp64_search(q, zh, tgt, Hp, gh[qi], rho, T, orig=True))
-        del tgt, zh
+        del zh
     return out
 
 
 def _run(g, mods, dev, arbitrate):
     """Steps the GPU along the golden.  arbitrate: 'all' runs the fp64 oracle before every step,
-    'lazy' only for steps whose exponents differ from the reference's.  Every step also gets the
+    'lazy' only for steps whose exponents differ from the reference's, 'none' never (the global
+    C5 problem: its fp64 state would not fit beside the library's).  Every step also gets the
     same-input fp64 search (_same_input_fp64)."""
     from admm_amd import _native as N
     model, opt = _optimizer(g, mods, dev)
@@ -98,18 +113,23 @@ def _run(g, mods, dev, arbitrate):
         zc = torch.empty(4, B * T, H, device=dev)
         assert N.load().admm_debug_workspace(opt._ctx, 0, N.ptr(zc), zc.numel() * 4, N.stream_handle(dev)) == 1
         W0 = {k: p.detach().clone() for k, p in model.named_parameters()}
-        S = {k: v.clone() for k, v in opt.gates.items()}
-        L = {k: v.clone() for k, v in opt.duals.items()}
+        if arbitrate == 'none':
+            S = L = None
+            pre = (zc, W0, _pre_targets(g, opt, dev))
+        else:
+            S = {k: v.clone() for k, v in opt.gates.items()}
+            L = {k: v.clone() for k, v in opt.duals.items()}
+            pre = (zc, W0, S, L)
         full = _full_fp64(g, W0, S, L, dev) if arbitrate == 'all' else None
         opt.step()
         st = opt.last_step_stats()
         assert st['unresolved'] == 0 and st['nonfinite'] == 0, (s, st)
         ks = [st['k'][n] for n in names]
         ref = g.ks(s)
-        same = _same_input_fp64(g, opt, (zc, W0, S, L), gx, gh, model, dev)
-        if full is None and ks != ref:
+        same = _same_input_fp64(g, opt, pre, gx, gh, model, dev)
+        if full is None and ks != ref and arbitrate != 'none':
             full = _full_fp64(g, W0, S, L, dev)
-        del zc, S, L
+        del zc, S, L, pre
         eps = None
         if full is not None:   # how far the library's G is from the fp64 oracle's (fp32 state rounding)
             mine = [gx[i // 2] if i % 2 == 0 else gh[i // 2] for i in range(8)]
@@ -151,7 +171,7 @@ def _write(name, recs, g):
 def test_fullsize_matches_reference(name, dev):
     g = Golden(name)
     mods = _load_mods()
-    recs = _run(g, mods, dev, arbitrate='all' if name == 'c3' else 'lazy')
+    recs = _run(g, mods, dev, arbitrate={'c3': 'all', 'c5g': 'none'}.get(name, 'lazy'))
     _write(name, recs, g)
     for r in recs:
         s = r['step']
@@ -159,7 +179,7 @@ def test_fullsize_matches_reference(name, dev):
         for n, d in r['wdiff'].items():
             assert d <= W_RTOL, (s, n, d)
         for i, (a, b) in enumerate(zip(r['k'], r['ref_k'])):
-            if a == b:
+            if a == b or r['fp64'] is None:   # (no full fp64 step: the same-input check below decides)
                 continue
             # the reference decided differently: the fp64 oracle from the GPU's own pre-step state
             # decides, up to the direction's own uncertainty -- G is a sum of residuals that the

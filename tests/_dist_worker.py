@@ -41,7 +41,7 @@ def main():
     from parameters import example_parameter_dictionary
     pd = example_parameter_dictionary['GoogleStock']
     per, T, D, H = (int(v) for v in os.environ.get('ADMM_DIST_SHAPE', '256,8,4,32').split(','))
-    Bg, steps = per * world, 3
+    Bg, steps = per * world, int(os.environ.get('ADMM_DIST_STEPS', '3'))
     g = torch.Generator().manual_seed(1234)
     x = torch.rand(Bg, T, D, generator=g)
     y = 0.8 * x.mean((1, 2)).unsqueeze(1) + 0.1 * torch.rand(Bg, 1, generator=g)

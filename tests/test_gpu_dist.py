@@ -19,12 +19,12 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _launch(world, backend, shape, variant='admm'):
+def _launch(world, backend, shape, variant='admm', extra_env=None):
     cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', f'--nproc-per-node={world}',
            '--master-addr=127.0.0.1', f'--master-port={_free_port()}',
            os.path.join(ROOT, 'tests', '_dist_worker.py')]
     env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY='0', ADMM_DIST_BACKEND=backend, ADMM_DIST_SHAPE=shape,
-               ADMM_DIST_VARIANT=variant, OMP_NUM_THREADS='4')
+               ADMM_DIST_VARIANT=variant, OMP_NUM_THREADS='4', **(extra_env or {}))
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env)
     out = r.stdout + r.stderr
     assert r.returncode == 0 and 'DIST OK' in out, out[-3000:]
@@ -37,6 +37,12 @@ def test_rccl_world1_matches_single_process():
 
 def test_rccl_world1_fast_path():
     _launch(1, 'nccl', '512,6,16,256')
+
+
+def test_rccl_world1_step_graph():
+    """ADMM_GRAPH=1 with RCCL: the steady-state step, its all-reduces included, captured into one HIP
+    graph and replayed (the worker steps enough times to replay it)."""
+    _launch(1, 'nccl', '512,6,16,256', extra_env={'ADMM_GRAPH': '1', 'ADMM_DIST_STEPS': '6'})
 
 
 @pytest.mark.parametrize('shape,variant', [

@@ -135,8 +135,8 @@ struct AdmmCtx {
   bool atr_f16 = true;
   float* range = nullptr;
   bool range_valid = false, x1_valid = false;
-  // column-split sweep (strong-scaling ranks, sweep_rows_nc > 1): h_t hand-off counters per row block
-  unsigned* xcnt = nullptr;
+  // column-split sweep (strong-scaling ranks, sweep_rows_nc > 1): the h_t hand-off granules
+  float* xbuf = nullptr;
   // pass 0 of a gate whose last exponent was past the first window also sums the per-candidate
   // elements' polynomial, so the exponents past it are decided without pass 1 (ADMM_P16=0: off)
   bool p16 = true;
@@ -445,9 +445,9 @@ int stage_sweep(AdmmCtx* c, hipStream_t s) {
     }
     sa.lamh_nz = c->lamh_known && c->lamh_skip ? c->lamh_nz : nullptr;
     sa.range = c->range;   // zeroed by this step's h-stage k_reduce_g
-    sa.xcnt = c->xcnt;     // zeroed by k_sweep_wt (column split only)
+    sa.xbuf = c->xbuf;     // zeroed by k_sweep_wt (column split only)
     sa.fail = &c->stats->nonfinite;   // a hand-off that timed out makes the step's results invalid
-    launch_sweep_wt(g, w, c->swt, s, c->xcnt);
+    launch_sweep_wt(g, w, c->swt, s, c->xbuf);
     launch_sweep_rows(g, c->swt, c->hp, sa, s);
   } else {
     // Samples are independent across the sweep: two halves on two streams run their
@@ -599,7 +599,7 @@ int admm_create(const AdmmDims* dims, const AdmmParams* params, int device, Admm
       (rc = dalloc(&c->Gy, (size_t)g.H * g.O)) || (rc = dalloc(&c->ht_part, (size_t)c->ht_nblk * kHTSums)) ||
       (rc = dalloc(&c->ht_sums, kHTSums)) || (rc = dalloc(&c->stats, 1)) || (rc = dalloc(&c->lamh_nz, 1)) || (rc = dalloc(&c->force_dev, 9)) || (rc = dalloc(&c->range, 8)) ||
       (c->sweep_rows && (rc = dalloc(&c->swt, sweep_wt_floats(g)))) ||
-      (c->sweep_rows && sweep_rows_nc(g) > 1 && cus >= kSweepCUs && (rc = dalloc(&c->xcnt, sweep_xcnt_words(g)))) ||
+      (c->sweep_rows && sweep_rows_nc(g) > 1 && cus >= kSweepCUs && (rc = dalloc(&c->xbuf, sweep_xbuf_bytes(g) / 4))) ||
       (c->split3 && (rc = dalloc(&c->gimg, split3_gimg_floats(g)))) ||
       (c->spec_x && ((rc = dalloc(&c->zx, 4 * plane)) || (rc = dalloc(&c->kpred, 4)))) ||
       (c->gx_nblk > 0 && (rc = dalloc(&c->gx_slab, (size_t)c->gx_nblk * 4 * g.D * g.H)))) {
@@ -636,7 +636,7 @@ int admm_destroy(AdmmCtx* c) {
   if (!c) return ADMM_OK;
   DeviceGuard dg_(c->device);
   void* ptrs[] = {c->zc, c->tgt, c->R, c->Q, c->G, c->dW, c->gslab, c->tr_part, c->tr_sums, c->tr_poly, c->found, c->pick,
-                  c->U, c->wy_slab, c->Gy, c->ht_part, c->ht_sums, c->stats, c->swt, c->gimg, c->zx, c->kpred, c->gx_slab, c->lamh_nz, c->force_dev, c->range, c->xcnt};
+                  c->U, c->wy_slab, c->Gy, c->ht_part, c->ht_sums, c->stats, c->swt, c->gimg, c->zx, c->kpred, c->gx_slab, c->lamh_nz, c->force_dev, c->range, c->xbuf};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   if (c->comm) ncclCommDestroy(c->comm);

@@ -291,6 +291,13 @@ __device__ __forceinline__ void range_max(float* dst, float v) {
   if ((threadIdx.x & 63) == 0) atomicMax(reinterpret_cast<unsigned*>(dst), __float_as_uint(v));
 }
 
+#ifdef SR_CS_TIMING   // tools/kbench: per-t phase timestamps of the column-split sweep's workgroup 0
+__device__ unsigned long long g_cs_t[64][12];
+#define CS_STAMP(t, e) do { if (blockIdx.x == 0 && (threadIdx.x & 63) == 0 && (t) < 64) g_cs_t[t][e] = wall_clock64(); } while (0)
+#else
+#define CS_STAMP(t, e) do { } while (0)
+#endif
+
 constexpr int SR_ROWS = 32, SR_THREADS = 512;
 #ifdef SR_TIMING
 __device__ unsigned long long g_sr_wait[2048][2];   // per workgroup: cycles the producer / consumer wave 0 waited at barriers
@@ -343,12 +350,12 @@ __global__ __launch_bounds__(kThreads) void k_sweep_wt16(int D, int H, int XC, W
 }
 
 __global__ __launch_bounds__(kThreads) void k_sweep_wt(int D, int H, int XC, Weights w, bf16x8* __restrict__ wt,
-                                                         unsigned* __restrict__ xcnt, int nx) {
+                                                         uint4* __restrict__ xbuf, int nx) {
   const int NT = H / 32, KC2 = XC + 2 * NT, XK = 16 * XC;
   const int total = 4 * NT * KC2 * 64;
-  // the column-split sweep's hand-off counters start every launch at 0 (this kernel runs right
+  // the column-split sweep's h_t granules start every launch with tag 0 (this kernel runs right
   // before it on the stream)
-  for (int i = blockIdx.x * kThreads + threadIdx.x; i < nx; i += gridDim.x * kThreads) xcnt[i] = 0u;
+  for (int i = blockIdx.x * kThreads + threadIdx.x; i < nx; i += gridDim.x * kThreads) xbuf[i] = make_uint4(0u, 0u, 0u, 0u);
   for (int i = blockIdx.x * kThreads + threadIdx.x; i < total; i += gridDim.x * kThreads) {
     const int lane = i & 63, c = (i >> 6) % KC2, n = (i / (64 * KC2)) % NT, q = i / (64 * KC2 * NT);
     const int jj = 32 * n + (lane & 31), h = lane >> 5;
@@ -383,14 +390,14 @@ __global__ __launch_bounds__(kThreads) void k_sweep_wt(int D, int H, int XC, Wei
 // NC > 1 (ROWS = 32, the strong-scaling path: few rows per GPU): the column-split sweep.  Workgroup
 // (rb, cg) owns the 32 rows of row block rb and the NTC = NT / NC column tiles cg NTC .. of every t,
 // so that B = 1024 rows fill 32 x 8 = 256 CUs instead of 32.  [x_t | h_{t-1}] still lives whole in
-// each workgroup's LDS; the NC workgroups of a row block exchange h_t through memory once per t:
-// the h_t stores are write-through (sc1), every consumer wave drains them, the last of the four
-// adds to its row block's counter (agent scope), and before the producer may start the h chunks of
-// t + 1 one consumer wave polls that counter to NC t; then the consumer waves read the other
-// workgroups' columns of h_t with sc1 loads into the A image (the R1 hand-off of
-// cdna_hip_programming.md Guideline 16, with sc1 loads in place of the acquire).  The counters
-// (a.xcnt, one per row block) are zeroed by k_sweep_wt before every launch; all workgroups must be
-// resident at once (the host checks the grid against the CUs), and every spin is bounded.
+// each workgroup's LDS; the NC workgroups of a row block exchange h_t through memory once per t as
+// 8-byte granules {h value, tag t} (cdna_hip_programming.md Guideline 16, R2: the data is the flag):
+// each consumer thread publishes its four h values with two 16-byte write-through (sc1) stores as
+// soon as they are computed, and before the producer may start the h chunks of t + 1 the consumer
+// waves re-read the other groups' granules (sc1 loads) until every tag is t, then split them into
+// the A image.  No drain, counter or fence.  The granule buffer (a.xbuf) is zeroed by k_sweep_wt
+// before every launch; all workgroups must be resident at once (the host checks the grid against
+// the CUs), and every spin is bounded.
 template <int NT, int XC, bool GX, int ROWS = 32, int NC = 1>
 __global__ __launch_bounds__(SR_THREADS) void k_sweep_rows(Geom g, const bf16x8* __restrict__ wt, Hyper hp,
                                                             SweepT a) {
@@ -406,10 +413,6 @@ __global__ __launch_bounds__(SR_THREADS) void k_sweep_rows(Geom g, const bf16x8*
   // GXC: per step parity, consumer wave and gate, the four-row sums of the tile's TW columns
   __shared__ __attribute__((aligned(16))) float Px[GXC ? 2 : 1][GXC ? 4 : 1][GXC ? 4 : 1][GXC ? TW : 1];
   __shared__ float Rg[GXC ? 5 * 256 : 1];   // GXC: the consumer threads' running range maxima
-  // NC > 1: [0] consumer waves that have drained their h_t stores (4 per t), [1] last t whose h from
-  // the other groups of the row block may be read
-  __shared__ int xsync[2];
-  if (NC > 1 && threadIdx.x < 2) xsync[threadIdx.x] = 0;
   const int T = g.T, D = g.D;
   // NC > 1: block b -> (row block rb, column group cg); the NC groups of a row block are blocks
   // b = x + 8 (NC i + cg), one XCD's under the observed round-robin placement (speed only)
@@ -562,7 +565,9 @@ __global__ __launch_bounds__(SR_THREADS) void k_sweep_rows(Geom g, const bf16x8*
         const int G = G0 + u;
         if (G < total) {
           const int t = G / GTC + 1, r = G - (t - 1) * GTC, nl = r / KC2, cc = r - nl * KC2;
+          if (nl == 0 && cc == 0 && q == 0) CS_STAMP(t, 8);
           if (nl == 0 && cc == XC) SR_SYNC();   // mid-step: all of h_{t-1} is in this A buffer
+          if (nl == 0 && cc == XC && q == 0) CS_STAMP(t, 9);
           const __bf16* A = &Ab[t & 1][c * AST + 8 * kh];
           const bf16x8 a0 = *reinterpret_cast<const bf16x8*>(A + 16 * cc);
           const bf16x8 a1 = *reinterpret_cast<const bf16x8*>(A + AP + 16 * cc);
@@ -582,6 +587,7 @@ __global__ __launch_bounds__(SR_THREADS) void k_sweep_rows(Geom g, const bf16x8*
 #pragma unroll
             for (int rr = 0; rr < 16; ++rr) Z[acc_row(rr, lane) * 32] = acc[rr];
             acc = f32x16{};
+            if (q == 0) CS_STAMP(t, 10);
             SR_SYNC();   // end of step
             if constexpr (GX)
               if (st >= 1) gx_fold((st - 1) & 1);
@@ -775,48 +781,59 @@ __global__ __launch_bounds__(SR_THREADS) void k_sweep_rows(Geom g, const bf16x8*
     }
   };
 
-  // NC > 1: publish this group's h_t (sc1 stores, drained by every consumer wave, the last of the
-  // four adds to the row block's counter), wait until the NC groups have published, then read the
-  // other groups' columns of h_t with sc1 loads into the A image of t + 1 (split3, as put_a).
+  // NC > 1: the h_t granules (see the kernel's comment).  rX spans the padded row blocks' granules.
+  const __amdgpu_buffer_rsrc_t rX = __builtin_amdgcn_make_buffer_rsrc(
+      NC > 1 ? a.xbuf : a.zc, 0, NC > 1 ? (uint32_t)((rb + 1) * 32 * H * 8) : 0u, kBufWord3);
+  // publish: this thread's four h_t values of tile n as two 16-byte granule pairs
+  auto publish = [&](int t, int n, f32x4 h) {
+    const float tg = __uint_as_float((unsigned)t);
+    const uint32_t go = (uint32_t)(((rb * 32 + row) * H + TW * n + j4) * 8);
+    buf_st4<16>(rX, go, f32x4{h[0], tg, h[1], tg});
+    buf_st4<16>(rX, go + 16, f32x4{h[2], tg, h[3], tg});
+  };
+  // read the other groups' columns of h_t once every granule carries tag t, into the A image of t + 1
   auto exchange = [&](int t) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's h_t stores have completed
-    if (lane == 0) {
-      const int old = atomicAdd(&xsync[0], 1);
-      if (old == 4 * t - 1) __hip_atomic_fetch_add(a.xcnt + rb, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    if (ct < 64) {   // one wave polls the counter (relaxed, agent scope: an sc1 load), bounded
-      const unsigned want = (unsigned)(NC * t);
-      for (unsigned spins = 0; __hip_atomic_load(a.xcnt + rb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < want;) {
-        if (++spins > (1u << 24)) {   // ~0.5 s: a group never arrived (not resident?) -- give up, flagged
-          if (lane == 0 && a.fail) atomicAdd(a.fail, 1);
-          break;
-        }
-        __builtin_amdgcn_s_sleep(1);
+    constexpr int OC = H - TW * NTC;               // other groups' columns
+    constexpr int NP = ROWS * OC / 2 / 256;        // 16-byte granule pairs per consumer thread
+    f32x4 gv[NP > 0 ? NP : 1];
+    auto addr = [&](int i, int& hr, int& col) {
+      const int f = ct + 256 * i;
+      hr = f / (OC / 2);
+      const int oc = 2 * (f % (OC / 2));
+      col = oc < TW * n0 ? oc : oc + TW * NTC;
+      return (uint32_t)(((rb * 32 + hr) * H + col) * 8);
+    };
+    const unsigned want = (unsigned)t;
+    for (unsigned spins = 0;; ++spins) {
+      bool ok = true;
+#pragma unroll
+      for (int i = 0; i < NP; ++i) {
+        int hr, col;
+        gv[i] = buf_ld4<kAuxL2>(rX, addr(i, hr, col));
       }
-      if (lane == 0) __hip_atomic_store(&xsync[1], t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    }
-    while (__hip_atomic_load(&xsync[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < t) __builtin_amdgcn_s_sleep(1);
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // keep the loads below the poll
-    constexpr int C4 = H / 4, NL = ROWS * C4 / 256;           // float4 of h_t per thread
-    f32x4 hv[NL];
 #pragma unroll
-    for (int i = 0; i < NL; ++i) {
-      const int f = ct + 256 * i, hr = f / C4, col = 4 * (f % C4);
-      const bool own = col >= TW * n0 && col < TW * (n0 + NTC);
-      const uint32_t off = (uint32_t)(((m0 + hr) * rs + (int64_t)t * H + col) * 4);
-      hv[i] = own ? f32x4{} : buf_ld4<kAuxL2>(rS[5], off);   // rows past r1 read 0
+      for (int i = 0; i < NP; ++i) ok &= __float_as_uint(gv[i][1]) == want && __float_as_uint(gv[i][3]) == want;
+      if (__all(ok)) break;
+      if (spins > (1u << 22)) {   // ~0.5 s: a group never published (not resident?) -- give up, flagged
+        if (lane == 0 && a.fail) atomicAdd(a.fail, 1);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
     }
+    if (ct == 0) CS_STAMP(t, 4);
 #pragma unroll
-    for (int i = 0; i < NL; ++i) {
-      const int f = ct + 256 * i, hr = f / C4, col = 4 * (f % C4);
-      if (col >= TW * n0 && col < TW * (n0 + NTC)) continue;
-      bf16x4 p0, p1, p2;
-      split3(hv[i], p0, p1, p2);
+    for (int i = 0; i < NP; ++i) {
+      int hr, col;
+      (void)addr(i, hr, col);
+      __bf16 p0, p1, p2;
       __bf16* d = &Ab[(t + 1) & 1][hr * AST + XK + col];
-      *reinterpret_cast<bf16x4*>(d) = p0;
-      *reinterpret_cast<bf16x4*>(d + AP) = p1;
-      *reinterpret_cast<bf16x4*>(d + 2 * AP) = p2;
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        split3(gv[i][2 * e], p0, p1, p2);
+        d[e] = p0; d[AP + e] = p1; d[2 * AP + e] = p2;
+      }
     }
+    if (ct == 0) CS_STAMP(t, 5);
   };
   // Tile operands are loaded one tile early (loading two tiles ahead measured no faster).
   // cring[0] is c_{t-1} of the tile being updated: popped at every tile, c_t pushed at the back.
@@ -856,6 +873,7 @@ __global__ __launch_bounds__(SR_THREADS) void k_sweep_rows(Geom g, const bf16x8*
       const unsigned long long ta_ = clock64();
 #endif
       const St4 cur = nxt;
+      if (NC > 1 && ct == 0) CS_STAMP(t, 0);
       const float xm = GXC && rok ? a.x[bx * T + (t - 1)] : 0.f;   // GXC (D == 1): x_t of this row
 #ifdef SR_TIMING
       asm volatile("" :: "v"(cur.f0), "v"(cur.g0), "v"(cur.c0), "v"(cur.h0), "v"(cur.li), "v"(cur.lf), "v"(cur.lg),
@@ -954,6 +972,8 @@ __global__ __launch_bounds__(SR_THREADS) void k_sweep_rows(Geom g, const bf16x8*
       asm volatile("" :: "v"(i1), "v"(f1), "v"(g1), "v"(o1), "v"(c1), "v"(h1), "v"(li), "v"(lf), "v"(lg), "v"(lo), "v"(lc));
       const unsigned long long tb_ = clock64();
 #endif
+      if constexpr (NC > 1)
+        if (!last) publish(t, n, h1);   // first: the other groups wait for it
       if (!last) {
         bf16x4 p0, p1, p2;
         split3(h1, p0, p1, p2);
@@ -962,10 +982,11 @@ __global__ __launch_bounds__(SR_THREADS) void k_sweep_rows(Geom g, const bf16x8*
         *reinterpret_cast<bf16x4*>(d + AP) = p1;
         *reinterpret_cast<bf16x4*>(d + 2 * AP) = p2;
       }
+      if (NC > 1 && ct == 0) CS_STAMP(t, 1);
       const uint32_t po = pofs + (uint32_t)(t * H + TW * n) * 4, zo4 = zofs + (uint32_t)((t - 1) * H + TW * n) * 4;
       buf_st4(rS[0], po, i1); buf_st4(rS[1], po, f1); buf_st4(rS[2], po, g1); buf_st4(rS[3], po, o1);
       buf_st4<0>(rS[4], po, c1);             // c_t: read by the next step's kernels
-      if (!last) buf_st4<NC == 1 ? 0 : 16>(rS[5], po, h1);   // NC > 1: write-through (sc1), handed off
+      if (!last) buf_st4<0>(rS[5], po, h1);
       buf_st4(rL[0], po, li); buf_st4(rL[1], po, lf); buf_st4(rL[2], po, lg); buf_st4(rL[3], po, lo);
       buf_st4(rL[4], po, lc);
       // one descriptor spans the 4 planes, so its record count cannot drop the stores of rows
@@ -982,10 +1003,12 @@ __global__ __launch_bounds__(SR_THREADS) void k_sweep_rows(Geom g, const bf16x8*
       const unsigned long long tc_ = clock64();
       if ((threadIdx.x & 63) == 0) { sr_comp += tb_ - ta_; sr_store += tc_ - tb_; }
 #endif
+      if (NC > 1 && ct == 0) CS_STAMP(t, 2);
       if (nl == NTC - 1 && !last) {
         load_x(t + 2);       // the producer's next tile is (t+1, n0)
         if constexpr (NC > 1) exchange(t);   // the other groups' columns of h_t into this A buffer
         SR_SYNC();           // its mid-step barrier: h_t is complete
+        if (NC > 1 && ct == 0) CS_STAMP(t, 6);
       }
       SR_SYNC();             // end of step
     }
@@ -3159,7 +3182,10 @@ int sweep_rows_nc(const Geom& g) {
   return 1;
 }
 
-int sweep_xcnt_words(const Geom& g) { return (int)(((g.B + 31) / 32 + 7) / 8 * 8); }
+int sweep_row_blocks_padded(const Geom& g) { return (int)(((g.B + 31) / 32 + 7) / 8 * 8); }
+
+// one 8-byte granule {h value, tag t} per (row, column) of every padded row block (k_sweep_rows NC > 1)
+size_t sweep_xbuf_bytes(const Geom& g) { return (size_t)sweep_row_blocks_padded(g) * 32 * g.H * 8; }
 
 static int sweep_xc(const Geom& g) { return sweep_r16(g) ? (g.D + 31) / 32 : (g.D + 15) / 16; }
 
@@ -3168,7 +3194,7 @@ size_t sweep_wt_floats(const Geom& g) {   // bf16x8 image, in float units
   return (size_t)4 * (g.H / 32) * (sweep_xc(g) + 2 * (g.H / 32)) * 3 * 64 * 4;
 }
 
-void launch_sweep_wt(const Geom& g, const Weights& w, float* wt, hipStream_t s, unsigned* xcnt) {
+void launch_sweep_wt(const Geom& g, const Weights& w, float* wt, hipStream_t s, void* xbuf) {
   const int xc = sweep_xc(g);
   if (sweep_r16(g)) {
     const int total = 4 * (g.H / 64) * (xc + g.H / 32) * 4 * 64;
@@ -3177,8 +3203,9 @@ void launch_sweep_wt(const Geom& g, const Weights& w, float* wt, hipStream_t s, 
   }
   const int NT = g.H / 32;
   const int total = 4 * NT * (xc + 2 * NT) * 64;
-  k_sweep_wt<<<cdiv64(total, kThreads), kThreads, 0, s>>>(g.D, g.H, xc, w, reinterpret_cast<bf16x8*>(wt), xcnt,
-                                                         xcnt ? sweep_xcnt_words(g) : 0);
+  k_sweep_wt<<<cdiv64(total, kThreads), kThreads, 0, s>>>(g.D, g.H, xc, w, reinterpret_cast<bf16x8*>(wt),
+                                                         reinterpret_cast<uint4*>(xbuf),
+                                                         xbuf ? (int)(sweep_xbuf_bytes(g) / 16) : 0);
 }
 
 template <int XC>
@@ -3196,9 +3223,9 @@ static void launch_sweep_rows_xc(const Geom& g, const bf16x8* wt, const Hyper& h
     }
     return;
   }
-  const int nc = a.xcnt ? sweep_rows_nc(g) : 1;
+  const int nc = a.xbuf ? sweep_rows_nc(g) : 1;
   if (nc > 1 && g.H == 256) {   // column split (strong-scaling ranks): padded row blocks x nc groups
-    dim3 grid((unsigned)(sweep_xcnt_words(g) * nc));
+    dim3 grid((unsigned)(sweep_row_blocks_padded(g) * nc));
     auto go = [&](auto ncv) {
       constexpr int NCV = decltype(ncv)::value;
       if (XC == 1 && a.gx_slab) k_sweep_rows<8, XC, true, 32, NCV><<<grid, SR_THREADS, 0, s>>>(g, wt, hp, a);
@@ -3528,6 +3555,24 @@ void launch_ht_apply(const Geom& g, const Hyper& hp, const Planes6& S, const Pla
   else k_ht_apply<0><<<ht_blocks(g), kThreads, 4 * g.O * sizeof(float), s>>>(g, hp, S, L, a, Ly, y, wy, sums, stats,
                                                                             status, force);
 }
+
+#ifdef SR_CS_TIMING
+extern "C" void cs_timing_dump(int T) {
+  unsigned long long h[64][12];
+  (void)hipMemcpyFromSymbol(h, HIP_SYMBOL(g_cs_t), sizeof h);
+  // wall_clock64: 100 MHz; per t: phase deltas in us, relative to the consumer's tile start
+  double acc[12] = {};
+  int n = 0;
+  for (int t = 2; t < T && t < 64; ++t, ++n)
+    for (int e = 1; e < 11; ++e) acc[e] += (double)(long long)(h[t][e] - h[t][0]) / 100.0;
+  printf("column-split sweep, workgroup 0, mean over t (us from the consumer's tile start): "
+         "computed %.2f stored %.2f drained %.2f polled %.2f exchanged %.2f mid %.2f | producer z start %.2f after mid %.2f tile end %.2f\n",
+         acc[1] / n, acc[2] / n, acc[3] / n, acc[4] / n, acc[5] / n, acc[6] / n, acc[8] / n, acc[9] / n, acc[10] / n);
+  double per_t = 0;
+  for (int t = 2; t < T - 1 && t < 63; ++t) per_t += (double)(long long)(h[t + 1][0] - h[t][0]) / 100.0;
+  printf("  consumer tile start to next tile start: %.2f us per t\n", per_t / (T - 3));
+}
+#endif
 
 }  // namespace admm
 

@@ -111,9 +111,9 @@ struct SweepT {
   // residual before phi'), [4] = max |h_{t-1}| over t = 1..T (the h stage's H_prev).  They bound
   // the h-side residual so k_atr3w can scale its fp16 operands (admm_split3.hip, kRange*)
   float* range;
-  // column-split sweep (sweep_rows_nc > 1): per row block h_t hand-off counters, zeroed by
-  // launch_sweep_wt; fail (nullable) counts hand-offs that timed out
-  unsigned* xcnt;
+  // column-split sweep (sweep_rows_nc > 1): the h_t granules of every padded row block
+  // (sweep_xbuf_bytes), zeroed by launch_sweep_wt; fail (nullable) counts hand-offs that timed out
+  void* xbuf;
   int* fail;
   int64_t r0, r1;           // sample rows [r0, r1) of this launch
 };
@@ -124,14 +124,15 @@ bool sweep_rows_ok(const Geom& g);
 bool sweep_rows_gx_ok(const Geom& g);   // ... and it can form the x stage's G_x partials (32-row tiles with D <= 16, 16-row tiles with D == 1)
 int sweep_rows_blocks(const Geom& g);   // its workgroups = its G_x slabs
 size_t sweep_wt_floats(const Geom& g);
-// column groups of the 32-row persistent sweep (1: row blocks only) and its hand-off counters
-// (SweepT::xcnt words); the column split needs every one of its workgroups resident at once:
-// kSweepCUs (one 140-KB-LDS workgroup per CU) bounds the grid, and the host checks the device
+// column groups of the 32-row persistent sweep (1: row blocks only), its padded row blocks and its
+// hand-off buffer (SweepT::xbuf); the column split needs every one of its workgroups resident at
+// once: kSweepCUs (one 140-KB-LDS workgroup per CU) bounds the grid, and the host checks the device
 constexpr int kSweepCUs = 256;
 int sweep_rows_nc(const Geom& g);
-int sweep_xcnt_words(const Geom& g);
-// xcnt (nullable): zeroed in the same launch (before a column-split sweep)
-void launch_sweep_wt(const Geom& g, const Weights& w, float* wt, hipStream_t s, unsigned* xcnt = nullptr);
+int sweep_row_blocks_padded(const Geom& g);
+size_t sweep_xbuf_bytes(const Geom& g);
+// xbuf (nullable): zeroed in the same launch (before a column-split sweep)
+void launch_sweep_wt(const Geom& g, const Weights& w, float* wt, hipStream_t s, void* xbuf = nullptr);
 void launch_sweep_rows(const Geom& g, const float* wt, const Hyper& hp, const SweepT& a, hipStream_t s);
 // flag |= 1 if lh[b][t][j] != 0 for some t in [1, T) (H % 4 == 0; flag zeroed by the caller)
 void launch_check_lamh(const Geom& g, const float* lh, int* flag, hipStream_t s);

@@ -29,6 +29,9 @@ static float* dev_random(size_t n, float lo, float hi, unsigned seed) {
 #ifdef SR_TIMING
 extern "C" void sr_timing_dump(int nblk);
 #endif
+#ifdef SR_CS_TIMING
+extern "C" void cs_timing_dump(int T);
+#endif
 static void timeit(const char* name, double bytes, double flops, const std::function<void()>& f) {
   hipEvent_t a, b;
   (void)hipEventCreate(&a); (void)hipEventCreate(&b);
@@ -140,7 +143,8 @@ int main(int argc, char** argv) {
          [&] { launch_atr(g, 1, x, S.p[5], R, slab, ns, s); });
   timeit("qgemm side1", f4 * (4 * n + BT * g.H), 2.0 * BT * g.H * 4 * g.H, [&] { launch_qgemm(g, 1, x, S.p[5], G, Q, s); });
   run_s3();
-  SweepT sw{x, S, L, zc, nullptr, nullptr, nullptr, 0, g.B};
+  SweepT sw{};
+  sw.x = x; sw.S = S; sw.L = L; sw.zc = zc; sw.r0 = 0; sw.r1 = g.B;
   timeit("sweep_t (t=5)", f4 * g.B * (g.D + 27.0 * g.H), 2.0 * g.B * (g.D + g.H) * 4 * g.H,
          [&] { launch_sweep_t(g, 5, w, hp, sw, s); });
   {
@@ -157,6 +161,19 @@ int main(int argc, char** argv) {
       float* wt; (void)hipMalloc(&wt, sweep_wt_floats(g) * 4);
       timeit("sweep_wt", 0, 0, [&] { launch_sweep_wt(g, w, wt, s); });
       timeit("sweep rows (1 launch)", sb, sf, [&] { launch_sweep_rows(g, wt, hp, sw, s); });
+      if (sweep_rows_nc(g) > 1) {   // the column-split sweep (counters zeroed by sweep_wt each time)
+        void* xc; (void)hipMalloc(&xc, sweep_xbuf_bytes(g));
+        int* fl; (void)hipMalloc(&fl, 4); (void)hipMemset(fl, 0, 4);
+        SweepT sc = sw;
+        sc.xbuf = xc;
+        sc.fail = fl;
+        timeit("sweep column split", sb, sf, [&] { launch_sweep_wt(g, w, wt, s, xc); launch_sweep_rows(g, wt, hp, sc, s); });
+        int f = 0; (void)hipMemcpy(&f, fl, 4, hipMemcpyDeviceToHost);
+        printf("column split: nc %d, hand-off timeouts %d\n", sweep_rows_nc(g), f);
+#ifdef SR_CS_TIMING
+        cs_timing_dump(g.T);
+#endif
+      }
 #ifdef SR_TIMING
       (void)hipDeviceSynchronize();
       sr_timing_dump((int)((g.B + 31) / 32));

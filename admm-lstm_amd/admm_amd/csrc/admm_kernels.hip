@@ -512,14 +512,16 @@ __global__ __launch_bounds__(SR_THREADS) void k_sweep_rows(Geom g, const bf16x8*
     static_assert(GTC >= U, "ring deeper than the chunk cycle");
     const int q = wave, c = lane & 31, kh = lane >> 5;
     const bf16x8* wq = wt + ((size_t)q * SG::GT + (size_t)n0 * KC2) * 3 * 64 + lane;   // [q][n][c]: contiguous
-    bf16x8 bq[U][3];
+    bf16x8 bq[NTC == 1 ? 1 : U][3];
+    if constexpr (NTC > 1) {
 #pragma unroll
-    for (int u = 0; u < U; ++u)
+      for (int u = 0; u < U; ++u)
 #pragma unroll
-      for (int p = 0; p < 3; ++p) bq[u][p] = wq[(u * 3 + p) * 64];
+        for (int p = 0; p < 3; ++p) bq[u][p] = wq[(u * 3 + p) * 64];
+    }
     f32x16 acc = {};
     f32x4 gx[NTC][2];
-    float xcur[8], xnext[8];
+    float xcur[8], xnext[NTC == 1 ? 1 : 8];
     int gxs = 0;
     auto load_gx_x = [&](int tn, float (&xv)[8]) {
 #pragma unroll
@@ -530,7 +532,9 @@ __global__ __launch_bounds__(SR_THREADS) void k_sweep_rows(Geom g, const bf16x8*
       }
     };
     auto gx_fold = [&](int buf) {
-      if ((gxs % NTC) == 0) {
+      if constexpr (NTC == 1) {
+        load_gx_x(gxs + 1, xcur);   // off the critical path: the producer then waits at mid-step
+      } else if ((gxs % NTC) == 0) {
 #pragma unroll
         for (int ks = 0; ks < 8; ++ks) xcur[ks] = xnext[ks];
         const int tn = gxs / NTC + 2;
@@ -555,8 +559,55 @@ __global__ __launch_bounds__(SR_THREADS) void k_sweep_rows(Geom g, const bf16x8*
     if constexpr (GX) {
 #pragma unroll
       for (int k = 0; k < NTC; ++k) gx[k][0] = gx[k][1] = f32x4{};
-      load_gx_x(1, xnext);
+      if constexpr (NTC > 1) load_gx_x(1, xnext);
     }
+    if constexpr (NTC == 1) {
+      // One column tile per group (NC = NT): the tile's whole B image, KC2 chunks x 3 pieces (204
+      // VGPRs at H = 256), stays in registers for the sweep -- the weights do not change during it, and
+      // streaming it from L2 per t kept the h chunks waiting on loads (4.5 us per t against 1.4 of
+      // MFMAs, kbench SR_CS_TIMING).  The x chunks (before the mid-step wait) are loaded per t.
+      constexpr int KH = KC2 - XC;
+      bf16x8 bres[KH][3], bx[XC][3];
+#pragma unroll
+      for (int cc = 0; cc < KH; ++cc)
+#pragma unroll
+        for (int p = 0; p < 3; ++p) bres[cc][p] = wq[((XC + cc) * 3 + p) * 64];
+#pragma unroll 1
+      for (int t = 1; t <= T; ++t) {
+        const __bf16* A = &Ab[t & 1][c * AST + 8 * kh];
+        if (q == 0) CS_STAMP(t, 8);
+#pragma unroll
+        for (int cc = 0; cc < XC; ++cc)
+#pragma unroll
+          for (int p = 0; p < 3; ++p) bx[cc][p] = wq[(cc * 3 + p) * 64];
+#pragma unroll
+        for (int cc = 0; cc < KC2; ++cc) {
+          if (cc == XC) {
+            SR_SYNC();   // mid-step: all of h_{t-1} is in this A buffer
+            if (q == 0) CS_STAMP(t, 9);
+          }
+          const bf16x8 a0 = *reinterpret_cast<const bf16x8*>(A + 16 * cc);
+          const bf16x8 a1 = *reinterpret_cast<const bf16x8*>(A + AP + 16 * cc);
+          const bf16x8 a2 = *reinterpret_cast<const bf16x8*>(A + 2 * AP + 16 * cc);
+          const bf16x8* b = cc < XC ? bx[cc < XC ? cc : 0] : bres[cc < XC ? 0 : cc - XC];
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a2, b[0], acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b[1], acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b[2], acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b[0], acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b[1], acc, 0, 0, 0);
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b[0], acc, 0, 0, 0);
+        }
+        const int st = t - 1;   // step index
+        float* Z = &Zb[st & 1][q * ZG + c];
+#pragma unroll
+        for (int rr = 0; rr < 16; ++rr) Z[acc_row(rr, lane) * 32] = acc[rr];
+        acc = f32x16{};
+        if (q == 0) CS_STAMP(t, 10);
+        SR_SYNC();   // end of step
+        if constexpr (GX)
+          if (st >= 1) gx_fold((st - 1) & 1);
+      }
+    } else {
     const int total = T * GTC;
 #pragma unroll 1
     for (int G0 = 0; G0 < total; G0 += U) {
@@ -595,6 +646,7 @@ __global__ __launch_bounds__(SR_THREADS) void k_sweep_rows(Geom g, const bf16x8*
         }
       }
     }
+    }   // NTC > 1
     __syncthreads();         // final step: the consumer drains the last tile
     if constexpr (GX) {
       gx_fold((T * NTC - 1) & 1);
@@ -782,12 +834,17 @@ __global__ __launch_bounds__(SR_THREADS) void k_sweep_rows(Geom g, const bf16x8*
   };
 
   // NC > 1: the h_t granules (see the kernel's comment).  rX spans the padded row blocks' granules.
+  // Two granule sets by the parity of t: a group overwrites the set of h_t only when it publishes
+  // h_{t+2}, after its exchange of h_{t+1}, which every other group published after reading all of
+  // h_t -- so no reader can miss a tag (with one set, a reader slowed past a group's h_{t+1} publish,
+  // e.g. behind its own plane stores, would spin on a tag that had already been overwritten).
+  const uint32_t xset = (uint32_t)(gridDim.x / NC) * 32 * H * 8;   // bytes per set
   const __amdgpu_buffer_rsrc_t rX = __builtin_amdgcn_make_buffer_rsrc(
-      NC > 1 ? a.xbuf : a.zc, 0, NC > 1 ? (uint32_t)((rb + 1) * 32 * H * 8) : 0u, kBufWord3);
+      NC > 1 ? a.xbuf : a.zc, 0, NC > 1 ? 2 * xset : 0u, kBufWord3);
   // publish: this thread's four h_t values of tile n as two 16-byte granule pairs
   auto publish = [&](int t, int n, f32x4 h) {
     const float tg = __uint_as_float((unsigned)t);
-    const uint32_t go = (uint32_t)(((rb * 32 + row) * H + TW * n + j4) * 8);
+    const uint32_t go = (t & 1) * xset + (uint32_t)(((rb * 32 + row) * H + TW * n + j4) * 8);
     buf_st4<16>(rX, go, f32x4{h[0], tg, h[1], tg});
     buf_st4<16>(rX, go + 16, f32x4{h[2], tg, h[3], tg});
   };
@@ -801,7 +858,7 @@ __global__ __launch_bounds__(SR_THREADS) void k_sweep_rows(Geom g, const bf16x8*
       hr = f / (OC / 2);
       const int oc = 2 * (f % (OC / 2));
       col = oc < TW * n0 ? oc : oc + TW * NTC;
-      return (uint32_t)(((rb * 32 + hr) * H + col) * 8);
+      return (t & 1) * xset + (uint32_t)(((rb * 32 + hr) * H + col) * 8);
     };
     const unsigned want = (unsigned)t;
     for (unsigned spins = 0;; ++spins) {
@@ -822,16 +879,16 @@ __global__ __launch_bounds__(SR_THREADS) void k_sweep_rows(Geom g, const bf16x8*
     }
     if (ct == 0) CS_STAMP(t, 4);
 #pragma unroll
-    for (int i = 0; i < NP; ++i) {
+    for (int i = 0; i < NP; ++i) {   // two adjacent columns per granule pair: 4-byte LDS writes
       int hr, col;
       (void)addr(i, hr, col);
-      __bf16 p0, p1, p2;
+      typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+      bf16x2 p0, p1, p2;
+      split3(f32x2{gv[i][0], gv[i][2]}, p0, p1, p2);
       __bf16* d = &Ab[(t + 1) & 1][hr * AST + XK + col];
-#pragma unroll
-      for (int e = 0; e < 2; ++e) {
-        split3(gv[i][2 * e], p0, p1, p2);
-        d[e] = p0; d[AP + e] = p1; d[2 * AP + e] = p2;
-      }
+      *reinterpret_cast<bf16x2*>(d) = p0;
+      *reinterpret_cast<bf16x2*>(d + AP) = p1;
+      *reinterpret_cast<bf16x2*>(d + 2 * AP) = p2;
     }
     if (ct == 0) CS_STAMP(t, 5);
   };
@@ -904,6 +961,19 @@ __global__ __launch_bounds__(SR_THREADS) void k_sweep_rows(Geom g, const bf16x8*
 #pragma unroll
       for (int k = 0; k + 1 < NTC; ++k) cring[k] = cring[k + 1];
       cring[NTC - 1] = c1;
+      // h_t first: the other groups (NC > 1) and the producer wait for it; the targets, maxima and
+      // residuals below are off that path
+      if constexpr (NC > 1)
+        if (!last) publish(t, n, h1);
+      if (!last) {
+        bf16x4 p0, p1, p2;
+        split3(h1, p0, p1, p2);
+        __bf16* d = An + TW * n;
+        *reinterpret_cast<bf16x4*>(d) = p0;
+        *reinterpret_cast<bf16x4*>(d + AP) = p1;
+        *reinterpret_cast<bf16x4*>(d + 2 * AP) = p2;
+      }
+      if (NC > 1 && ct == 0) CS_STAMP(t, 3);
       // lam/rho + S of the updated i, f, g, o: the next x stage's targets (tgt_quot, as k_resid_gx)
       f32x4 ti, tf, tg, to;
       if (hp.rinv_exact) {   // workgroup-uniform: 16 IEEE divisions per tile and thread saved
@@ -972,16 +1042,6 @@ __global__ __launch_bounds__(SR_THREADS) void k_sweep_rows(Geom g, const bf16x8*
       asm volatile("" :: "v"(i1), "v"(f1), "v"(g1), "v"(o1), "v"(c1), "v"(h1), "v"(li), "v"(lf), "v"(lg), "v"(lo), "v"(lc));
       const unsigned long long tb_ = clock64();
 #endif
-      if constexpr (NC > 1)
-        if (!last) publish(t, n, h1);   // first: the other groups wait for it
-      if (!last) {
-        bf16x4 p0, p1, p2;
-        split3(h1, p0, p1, p2);
-        __bf16* d = An + TW * n;
-        *reinterpret_cast<bf16x4*>(d) = p0;
-        *reinterpret_cast<bf16x4*>(d + AP) = p1;
-        *reinterpret_cast<bf16x4*>(d + 2 * AP) = p2;
-      }
       if (NC > 1 && ct == 0) CS_STAMP(t, 1);
       const uint32_t po = pofs + (uint32_t)(t * H + TW * n) * 4, zo4 = zofs + (uint32_t)((t - 1) * H + TW * n) * 4;
       buf_st4(rS[0], po, i1); buf_st4(rS[1], po, f1); buf_st4(rS[2], po, g1); buf_st4(rS[3], po, o1);
@@ -1004,6 +1064,8 @@ __global__ __launch_bounds__(SR_THREADS) void k_sweep_rows(Geom g, const bf16x8*
       if ((threadIdx.x & 63) == 0) { sr_comp += tb_ - ta_; sr_store += tc_ - tb_; }
 #endif
       if (NC > 1 && ct == 0) CS_STAMP(t, 2);
+      // (NC > 1: issuing these stores after the hand-off poll, so that the poll's loads do not
+      // retire behind them, measured slower: the stores then delay the mid-step barrier)
       if (nl == NTC - 1 && !last) {
         load_x(t + 2);       // the producer's next tile is (t+1, n0)
         if constexpr (NC > 1) exchange(t);   // the other groups' columns of h_t into this A buffer
@@ -3185,7 +3247,7 @@ int sweep_rows_nc(const Geom& g) {
 int sweep_row_blocks_padded(const Geom& g) { return (int)(((g.B + 31) / 32 + 7) / 8 * 8); }
 
 // one 8-byte granule {h value, tag t} per (row, column) of every padded row block (k_sweep_rows NC > 1)
-size_t sweep_xbuf_bytes(const Geom& g) { return (size_t)sweep_row_blocks_padded(g) * 32 * g.H * 8; }
+size_t sweep_xbuf_bytes(const Geom& g) { return (size_t)sweep_row_blocks_padded(g) * 32 * g.H * 8 * 2; }   // two sets
 
 static int sweep_xc(const Geom& g) { return sweep_r16(g) ? (g.D + 31) / 32 : (g.D + 15) / 16; }
 
@@ -3566,8 +3628,8 @@ extern "C" void cs_timing_dump(int T) {
   for (int t = 2; t < T && t < 64; ++t, ++n)
     for (int e = 1; e < 11; ++e) acc[e] += (double)(long long)(h[t][e] - h[t][0]) / 100.0;
   printf("column-split sweep, workgroup 0, mean over t (us from the consumer's tile start): "
-         "computed %.2f stored %.2f drained %.2f polled %.2f exchanged %.2f mid %.2f | producer z start %.2f after mid %.2f tile end %.2f\n",
-         acc[1] / n, acc[2] / n, acc[3] / n, acc[4] / n, acc[5] / n, acc[6] / n, acc[8] / n, acc[9] / n, acc[10] / n);
+         "published %.2f computed %.2f stored %.2f polled %.2f exchanged %.2f mid %.2f | producer z start %.2f after mid %.2f tile end %.2f\n",
+         acc[3] / n, acc[1] / n, acc[2] / n, acc[4] / n, acc[5] / n, acc[6] / n, acc[8] / n, acc[9] / n, acc[10] / n);
   double per_t = 0;
   for (int t = 2; t < T - 1 && t < 63; ++t) per_t += (double)(long long)(h[t + 1][0] - h[t][0]) / 100.0;
   printf("  consumer tile start to next tile start: %.2f us per t\n", per_t / (T - 3));

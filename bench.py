@@ -56,6 +56,7 @@ CONFIGS = {
     # strong-scaling rank of C3 at N = 8: 1024 of the 8192 samples (the per-rank step of the 8-GPU run)
     'c3s': (1024, 32, 16, 256, 'admm', 'uniform'),
 }
+CPU_BASELINE_OFF = {'c4g'}   # configs whose CPU baseline is skipped unless --cpu-baseline
 
 
 def make_data(gen: str, B: int, T: int, D: int, seed_offset: int = 0):
@@ -275,6 +276,9 @@ def main():
                     help='headline at N > 1: strong (the config global batch, default) or weak (its batch per rank)')
     ap.add_argument('--no-weak', action='store_true', help='N > 1: skip the extra weak-scaling measurement')
     ap.add_argument('--no-cpu-baseline', action='store_true')
+    # the CPU oracle runs the config's full batch: at C4g (65536 rows, 8x C3) four steps take ~15 min,
+    # so it is off there unless asked for
+    ap.add_argument('--cpu-baseline', action='store_true', help='time the CPU baseline even where it is off by default (c4g)')
     ap.add_argument('--cpu-steps', type=int, default=3, help='timed CPU-baseline steps after step 1 (median)')
     ap.add_argument('--profile-classes', default='sweep,trial,trial_h,trial_extra,atr_x,atr_h,qgemm_x,qgemm_h,resid,small')
     # rehearsal of the N > 1 path on a one-GPU box: every rank on device 0, torch.distributed over
@@ -436,7 +440,7 @@ def main():
 
     if rank == 0:
         cpu = None
-        if world == 1 and not args.no_cpu_baseline:
+        if world == 1 and not args.no_cpu_baseline and (args.cpu_baseline or args.config not in CPU_BASELINE_OFF):
             cpu = cpu_baseline(args.config, args.cpu_steps)
         out = {
             'metric': 'ADMM iters/sec at hidden=256, batch=8192, seq=32; 1/2/4/8-GPU scaling',

@@ -137,6 +137,7 @@ struct AdmmCtx {
   bool range_valid = false, x1_valid = false;
   // column-split sweep (strong-scaling ranks, sweep_rows_nc > 1): the h_t hand-off granules
   float* xbuf = nullptr;
+  bool cs_poison = false;   // test hook (ADMM_SWEEP_SPLIT_COLS=2)
   // pass 0 of a gate whose last exponent was past the first window also sums the per-candidate
   // elements' polynomial, so the exponents past it are decided without pass 1 (ADMM_P16=0: off)
   bool p16 = true;
@@ -448,6 +449,7 @@ int stage_sweep(AdmmCtx* c, hipStream_t s) {
     sa.xbuf = c->xbuf;     // zeroed by k_sweep_wt (column split only)
     sa.fail = &c->stats->nonfinite;   // a hand-off that timed out makes the step's results invalid
     launch_sweep_wt(g, w, c->swt, s, c->xbuf);
+    if (c->cs_poison && c->xbuf) sweep_poison_entry(g, c->xbuf, s);
     launch_sweep_rows(g, c->swt, c->hp, sa, s);
   } else {
     // Samples are independent across the sweep: two halves on two streams run their
@@ -571,9 +573,11 @@ int admm_create(const AdmmDims* dims, const AdmmParams* params, int device, Admm
   // the column-split sweep keeps all its workgroups resident at once: one per CU, kSweepCUs of them
   int cus = 0;
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) cus = 0;
-  {   // ADMM_SWEEP_SPLIT_COLS=0: row blocks only (test hook); default on
+  {   // ADMM_SWEEP_SPLIT_COLS=0: row blocks only; =2: the column split's entry count poisoned before
+      // every launch, so the gated row-block sweep does the work (test hooks); default on
     const char* e = std::getenv("ADMM_SWEEP_SPLIT_COLS");
     if (e && std::atoi(e) == 0) cus = 0;
+    c->cs_poison = e && std::atoi(e) == 2;
   }
   const size_t plane = (size_t)g.BT() * g.H;
   // the sweep's x-stage partials: persistent sweep, fast path, D <= 16, targets from the sweep

@@ -7,6 +7,7 @@
 //   output weight wy ................ admm.py:246-280, admm.no_dual_y.py:226-249
 //   h_T search, a, duals at T ....... admm.py:459-502, 532-546, admm.no_dual_y.py:414-456
 // Layouts: gates/duals [B][T+1][H] (the reference's), caches [4][B*T][H] (row = b*T + t-1).
+#include <cstdio>
 #include <cstdlib>
 
 #include "admm_dev.hpp"
@@ -398,6 +399,30 @@ __global__ __launch_bounds__(kThreads) void k_sweep_wt(int D, int H, int XC, Wei
 // the A image.  No drain, counter or fence.  The granule buffer (a.xbuf) is zeroed by k_sweep_wt
 // before every launch; all workgroups must be resident at once (the host checks the grid against
 // the CUs), and every spin is bounded.
+// Column-split entry consensus: the hand-off needs every workgroup of the grid resident at once.
+// Each workgroup counts itself in and waits (bounded by the wall clock) for the whole grid; one
+// that gives up poisons the count with a CAS against the value it last saw, so either the count
+// reaches the grid size (all run) or it is poisoned first (every workgroup, late ones included,
+// leaves before touching the state, and the row-block sweep launched next does the work instead).
+constexpr unsigned kSweepPoison = 0x40000000u;
+constexpr uint64_t kSweepArriveTicks = 200000;   // 2 ms of the 100 MHz wall clock
+__device__ __forceinline__ bool sweep_arrive(unsigned* ctl, unsigned n) {
+  unsigned v = __hip_atomic_fetch_add(ctl, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
+  const uint64_t t0 = wall_clock64();
+  for (;;) {
+    if (v >= kSweepPoison) return false;
+    if (v == n) return true;
+    if (wall_clock64() - t0 > kSweepArriveTicks) {
+      const unsigned old = atomicCAS(ctl, v, v | kSweepPoison);
+      if (old == v) return false;
+      v = old;
+      continue;
+    }
+    __builtin_amdgcn_s_sleep(4);
+    v = __hip_atomic_load(ctl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
 template <int NT, int XC, bool GX, int ROWS = 32, int NC = 1>
 __global__ __launch_bounds__(SR_THREADS) void k_sweep_rows(Geom g, const bf16x8* __restrict__ wt, Hyper hp,
                                                             SweepT a) {
@@ -414,6 +439,17 @@ __global__ __launch_bounds__(SR_THREADS) void k_sweep_rows(Geom g, const bf16x8*
   __shared__ __attribute__((aligned(16))) float Px[GXC ? 2 : 1][GXC ? 4 : 1][GXC ? 4 : 1][GXC ? TW : 1];
   __shared__ float Rg[GXC ? 5 * 256 : 1];   // GXC: the consumer threads' running range maxima
   const int T = g.T, D = g.D;
+  if constexpr (NC > 1) {
+    __shared__ int go_s;
+    if (threadIdx.x == 0) {
+      const size_t xset = (size_t)(gridDim.x / NC) * 32 * H * 8;   // the two granule sets, then the count
+      go_s = sweep_arrive(reinterpret_cast<unsigned*>(static_cast<char*>(a.xbuf) + 2 * xset), gridDim.x);
+    }
+    __syncthreads();
+    if (!go_s) return;
+  } else {
+    if (a.gate && *a.gate < kSweepPoison) return;   // the column split ran
+  }
   // NC > 1: block b -> (row block rb, column group cg); the NC groups of a row block are blocks
   // b = x + 8 (NC i + cg), one XCD's under the observed round-robin placement (speed only)
   const int rb = NC == 1 ? (int)blockIdx.x : (int)(blockIdx.x % 8) + 8 * (int)(blockIdx.x / (8 * NC));
@@ -3247,7 +3283,12 @@ int sweep_rows_nc(const Geom& g) {
 int sweep_row_blocks_padded(const Geom& g) { return (int)(((g.B + 31) / 32 + 7) / 8 * 8); }
 
 // one 8-byte granule {h value, tag t} per (row, column) of every padded row block (k_sweep_rows NC > 1)
-size_t sweep_xbuf_bytes(const Geom& g) { return (size_t)sweep_row_blocks_padded(g) * 32 * g.H * 8 * 2; }   // two sets
+void sweep_poison_entry(const Geom& g, void* xbuf, hipStream_t s) {
+  (void)hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(static_cast<char*>(xbuf) + sweep_xbuf_bytes(g) - 256),
+                          (int)kSweepPoison, 1, s);
+}
+// two granule sets, then the entry count (k_sweep_rows' sweep_arrive)
+size_t sweep_xbuf_bytes(const Geom& g) { return (size_t)sweep_row_blocks_padded(g) * 32 * g.H * 8 * 2 + 256; }
 
 static int sweep_xc(const Geom& g) { return sweep_r16(g) ? (g.D + 31) / 32 : (g.D + 15) / 16; }
 
@@ -3296,6 +3337,14 @@ static void launch_sweep_rows_xc(const Geom& g, const bf16x8* wt, const Hyper& h
     if (nc == 8) go(std::integral_constant<int, 8>{});
     else if (nc == 4) go(std::integral_constant<int, 4>{});
     else go(std::integral_constant<int, 2>{});
+    // the row-block sweep, in case the column split could not have its whole grid resident (its
+    // workgroups leave at once otherwise: one empty launch per step)
+    SweepT ar = a;
+    ar.gate = reinterpret_cast<const unsigned*>(static_cast<const char*>(a.xbuf) + sweep_xbuf_bytes(g) - 256);
+    ar.xbuf = nullptr;
+    dim3 rgrid(cdiv64(a.r1 - a.r0, SR_ROWS));
+    if (XC == 1 && a.gx_slab) k_sweep_rows<8, XC, true><<<rgrid, SR_THREADS, 0, s>>>(g, wt, hp, ar);
+    else k_sweep_rows<8, XC, false><<<rgrid, SR_THREADS, 0, s>>>(g, wt, hp, ar);
     return;
   }
   dim3 grid(cdiv64(a.r1 - a.r0, SR_ROWS));

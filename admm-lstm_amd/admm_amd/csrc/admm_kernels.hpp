@@ -115,6 +115,9 @@ struct SweepT {
   // (sweep_xbuf_bytes), zeroed by launch_sweep_wt; fail (nullable) counts hand-offs that timed out
   void* xbuf;
   int* fail;
+  // the row-block sweep launched after a column-split one (launch_sweep_rows): runs only if that
+  // launch found its workgroups not all resident and left without touching the state (nullable)
+  const unsigned* gate;
   int64_t r0, r1;           // sample rows [r0, r1) of this launch
 };
 void launch_sweep_t(const Geom& g, int t, const Weights& w, const Hyper& hp, const SweepT& a, hipStream_t s);
@@ -129,6 +132,9 @@ size_t sweep_wt_floats(const Geom& g);
 // once: kSweepCUs (one 140-KB-LDS workgroup per CU) bounds the grid, and the host checks the device
 constexpr int kSweepCUs = 256;
 int sweep_rows_nc(const Geom& g);
+// test hook: poison the column split's entry count in xbuf (after launch_sweep_wt zeroed it), so
+// that its launch leaves at once and the gated row-block sweep runs
+void sweep_poison_entry(const Geom& g, void* xbuf, hipStream_t s);
 int sweep_row_blocks_padded(const Geom& g);
 size_t sweep_xbuf_bytes(const Geom& g);
 // xbuf (nullable): zeroed in the same launch (before a column-split sweep)

@@ -913,7 +913,10 @@ def test_column_split_sweep_bit_identical(B, mods, dev, monkeypatch):
     8, 4 or 2 column groups per row block, h_t handed between the groups through memory once per t)
     against the row-block sweep (ADMM_SWEEP_SPLIT_COLS=0): the same products in the same order, so
     weights, exponents, gates, duals and the z cache are bitwise equal over four steps (with the
-    next x stage's G_x partials from the sweep).  B = 1000 and 300: padded row blocks."""
+    next x stage's G_x partials from the sweep).  B = 1000 and 300: padded row blocks.  Mode 2
+    (B = 1024, 300) poisons the column split's entry count before every launch, as when its grid
+    cannot be resident at once: its workgroups leave without touching the state and the gated
+    row-block sweep launched after it does the work."""
     from blocks.lstm import LSTM
     from parameters import example_parameter_dictionary
     from admm_amd import _native as N
@@ -924,7 +927,7 @@ def test_column_split_sweep_bit_identical(B, mods, dev, monkeypatch):
     x = torch.rand(B, T, D, generator=g).to(dev)
     y = (0.8 * x.mean((1, 2)).unsqueeze(1) + 0.1 * torch.rand(B, 1, generator=g).to(dev)).contiguous()
     out = []
-    for mode in ('0', '1'):
+    for mode in ('0', '1', '2') if B in (1024, 300) else ('0', '1'):
         monkeypatch.setenv('ADMM_SWEEP_SPLIT_COLS', mode)
         torch.manual_seed(0)
         m = LSTM(D, H, 1).to(dev)
@@ -941,9 +944,10 @@ def test_column_split_sweep_bit_identical(B, mods, dev, monkeypatch):
                                   + [v.flatten() for v in opt.gates.values()]
                                   + [v.flatten() for v in opt.duals.values()]), zc))
         del opt
-    assert out[0][0] == out[1][0]
-    assert torch.equal(out[0][1], out[1][1])
-    assert torch.equal(out[0][2], out[1][2])
+    for o in out[1:]:
+        assert out[0][0] == o[0]
+        assert torch.equal(out[0][1], o[1])
+        assert torch.equal(out[0][2], o[2])
 
 
 @pytest.mark.parametrize('shape', [(2048, 8, 16, 256), (1024, 4, 16, 256), (300, 3, 16, 64)])

@@ -381,10 +381,12 @@ int stage_weights(AdmmCtx* c, int side, hipStream_t s) {
   sa.pick = c->pick;
   sa.stats = c->stats;
   sa.force = c->force_on ? c->force_dev : nullptr;
-  const int nblk = fast ? stream_blocks(g) : c->nblk_trial;
+  const int nblk = fast ? trial_fast_blocks(g, side) : c->nblk_trial;
   // the row-pair trial kernel (H % 256 == 0) writes one partial per (block, column block)
   const int nred = fast && side == 0 && trial_mx_ok(g) ? nblk * (g.H / 128)
                    : fast && trial_rows_ok(g) ? nblk * (g.H / 256) : nblk;
+  if (nred > c->nblk_trial)   // the partial buffer holds nblk_trial per slot and window
+    return fail(ADMM_ESTATE, "trial partials %d exceed the %d allocated", nred, c->nblk_trial);
   // pass 0, then the tail (windows 1 .. kMaxPasses - 1 in one launch, one selection, one
   // all-reduce) for the gates pass 0 left undecided -- with the polynomial past the window
   // (hint, k_reduce_g) that is rare, and the tail's workgroups exit at once

@@ -1860,14 +1860,42 @@ __device__ __forceinline__ void trial_pair_fold(float (&acc)[kSlots], const f32x
 __device__ __forceinline__ int pass_lo(int pass) { return pass == kTailPass ? 1 : pass; }
 __device__ __forceinline__ int pass_hi(int pass) { return pass == kTailPass ? kMaxPasses : pass + 1; }
 
+// Per-slot wave sums of v[0 .. N) (N <= 64): lane s ends with slot s's sum over the wave's 64 lanes,
+// bitwise equal to wave_sum(v[s]) -- the same pairs of partial sums, lanes 32 apart first, and IEEE
+// addition commutes -- in 63 shuffles instead of 6 N: at each butterfly stage a lane keeps the half
+// of its slots that its lane bit selects and sends the other half to its partner.  (k_select's 38
+// slots through wave_sum took 13 of its 18-19 us, tools/kbench "sel"; every trial workgroup's
+// epilogue reduces the same 38 slots.)
+template <typename T, int N>
+__device__ __forceinline__ T wave_sum_slots(T (&v)[N]) {   // in place: v is consumed
+  static_assert(N <= 64, "one slot per lane");
+  const int lane = threadIdx.x & 63;
+  {
+    const bool up = lane & 32;
+#pragma unroll
+    for (int s = 0; s < 32; ++s) {
+      const T lo = s < N ? v[s] : T(0), hi = s + 32 < N ? v[s + 32] : T(0);
+      if (s < N) v[s] = (up ? hi : lo) + __shfl_xor(up ? lo : hi, 32, kWave);
+    }
+  }
+#pragma unroll
+  for (int wdt = 16; wdt >= 1; wdt /= 2) {
+    const bool b = lane & wdt;
+#pragma unroll
+    for (int s = 0; s < wdt; ++s)
+      if (s < N) {
+        const T lo = v[s], hi = s + wdt < N ? v[s + wdt] : T(0);
+        v[s] = (b ? hi : lo) + __shfl_xor(b ? lo : hi, wdt, kWave);
+      }
+  }
+  return v[0];
+}
+
 __device__ __forceinline__ void trial_block_store(float (&acc)[kSlots], double* part, int q, int blk, int nblk) {
   __shared__ double red[4][kSlots];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-#pragma unroll
-  for (int k = 0; k < kSlots; ++k) {
-    const float s = wave_sum(acc[k]);
-    if (lane == 0) red[w][k] = (double)s;
-  }
+  const float s = wave_sum_slots(acc);   // lane k: slot k (wave_sum's bits)
+  if (lane < kSlots) red[w][lane] = (double)s;
   __syncthreads();
   if (threadIdx.x < kSlots) {
     const int k = threadIdx.x;
@@ -2757,11 +2785,8 @@ __global__ __launch_bounds__(kThreads) void k_select(Geom g, Hyper hp, SelectArg
 #pragma unroll
       for (int k = 0; k < kSlots; ++k) acc[k] += p[(int64_t)k * a.nred + i];
     }
-#pragma unroll
-    for (int k = 0; k < kSlots; ++k) {
-      const double v = wave_sum(acc[k]);
-      if (lane == 0) red[w][k] = v;
-    }
+    const double v = wave_sum_slots(acc);
+    if (lane < kSlots) red[w][lane] = v;
     __syncthreads();
     if (tid < kSlots) sums[tid] = (red[0][tid] + red[1][tid]) + (red[2][tid] + red[3][tid]);
   } else if (tid < kSlots) {
@@ -3550,6 +3575,21 @@ void launch_apply_fix(const Geom& g, const float* x, const float* dW, const floa
 }
 
 bool trial_rows_ok(const Geom& g) { return g.H % 256 == 0; }
+
+// workgroups per gate (and column block) of the fast trial passes.  Each walks the rows with a
+// stride of that many tiles, so few rows per GPU leave each workgroup few tiles to amortise its
+// setup and its epilogue (the 38-slot block reduction) over: at B = 1024 the x trials (k_trial_mx)
+// take 111 / 99 / 92 us with 512 / 256 / 128 workgroups (tools/kbench "tr", KB_NB), so they get at
+// least 16 tiles per workgroup; at B = 8192 (512: 513 us, 256: 509) and for the h trials the
+// streaming count stays.  Never more than stream_blocks(g): the partial buffer is sized for it.
+int trial_fast_blocks(const Geom& g, int side) {
+  const int sb = stream_blocks(g);
+  if (side == 0 && trial_mx_ok(g)) {
+    const int64_t nb = (g.BT() + 15) / 16 / 16;   // >= 16 tiles per workgroup
+    return (int)std::min<int64_t>(sb, std::max<int64_t>(64, nb));
+  }
+  return sb;
+}
 
 bool trial_mx_ok(const Geom& g) {   // else (a gate plane past 2 GB) the x side runs on k_trial_rows (VALU q)
   // 32-bit buffer offsets within one gate plane

@@ -225,6 +225,7 @@ bool trial_rows_ok(const Geom& g);
 // H % 256 == 0, D <= 16: the x-side trial passes run on the matrix cores (k_trial_mx) over
 // H/128 column groups, writing stream_blocks(g) * H/128 partials per slot
 bool trial_mx_ok(const Geom& g);
+int trial_fast_blocks(const Geom& g, int side);   // the fast trial passes' workgroups per gate (nblk)
 
 // after the x stage (fast path): zc += X dWx
 void launch_apply_dwx(const Geom& g, const float* x, const float* dW, float* zc, hipStream_t s);

@@ -76,7 +76,7 @@ int main(int argc, char** argv) {
   int* found; (void)hipMalloc(&found, 16); (void)hipMemset(found, 0, 16);
   hipStream_t s = 0;
   const double f4 = 4.0;
-  const int nb = stream_blocks(g);
+  const int nb = getenv("KB_NB") ? atoi(getenv("KB_NB")) : stream_blocks(g);   // trial grid override (A/B)
   auto run_s3 = [&] {
   if (split3_ok(g)) {
     // split-bf16 h-stage GEMMs: timing, and agreement with the f32-MFMA kernels above
@@ -114,6 +114,33 @@ int main(int argc, char** argv) {
   };
   const std::string mode = argc > 2 ? argv[2] : "";
   if (mode == "s3") { run_s3(); return 0; }
+  if (mode == "sel") {   // k_select of pass 0 (single process: it reduces the trial partials itself)
+    DevStats* st; (void)hipMalloc(&st, sizeof(DevStats)); (void)hipMemset(st, 0, sizeof(DevStats));
+    int* fl; (void)hipMalloc(&fl, 64); (void)hipMemset(fl, 0, 64);
+    int* pick; (void)hipMalloc(&pick, 16);
+    double* poly; (void)hipMalloc(&poly, 4 * kPolyN * 8);
+    for (int side = 0; side < 2; ++side) {
+      const int nred = side == 0 ? nb * (g.H / 128) : nb * (g.H / 256);
+      (void)hipMemset(part, 0, (size_t)4 * kTrialSlots * nred * 8);
+      SelectArgs sa{};
+      sa.side = side; sa.pass = 0; sa.last_pass = kMaxPasses - 1;
+      sa.part = part; sa.nred = nred; sa.poly = poly;
+      sa.G = G;
+      for (int q = 0; q < 4; ++q) sa.W[q] = W[side * 4 + q];
+      sa.dW = side == 0 ? dW : nullptr;
+      sa.found_in = fl; sa.found_out = fl + 4; sa.pick = pick; sa.stats = st;
+      char nm[64]; snprintf(nm, sizeof nm, "select side %d (nred %d)", side, nred);
+      for (int r = 0; r < 3; ++r) timeit(nm, 0, 0, [&] { launch_select(g, hp, sa, s); });
+    }
+    return 0;
+  }
+  if (mode == "tr") {   // the two pass-0 trial kernels alone
+    for (int r = 0; r < 3; ++r) {
+      timeit("trial_fast side0", f4 * 2 * 4 * n, 0, [&] { launch_trial_fast(g, 0, 0, zc, tgt, nullptr, x, G, found, part, nb, s); });
+      timeit("trial_fast side1", f4 * 3 * 4 * n, 0, [&] { launch_trial_fast(g, 1, 0, zc, tgt, Q, x, dW, found, part, nb, s); });
+    }
+    return 0;
+  }
   if (mode == "q") {   // Q = Hprev G (k_qgemm_res at H = 256, else k_qgemm3<1>)
     float* gimg; (void)hipMalloc(&gimg, split3_gimg_floats(g) * 4);
     float* Q3; (void)hipMalloc(&Q3, (size_t)4 * n * 4);

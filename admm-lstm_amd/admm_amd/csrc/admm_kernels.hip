@@ -3299,7 +3299,9 @@ int sweep_rows_blocks(const Geom& g) { return (int)((g.B + (sweep_r16(g) ? 15 : 
 int sweep_rows_nc(const Geom& g) {
   if (sweep_r16(g) || g.H != 256 || !sweep_rows_ok(g)) return 1;
   const int64_t nrb = (g.B + 31) / 32, pad = (nrb + 7) / 8 * 8;
-  if (nrb >= 128) return 1;
+  // (at 4096 rows, 128 row blocks, two groups still pay: 1.07 against 1.39 ms for the row-block sweep;
+  // 2048 rows, four groups: 0.63 against 1.31 ms; tools/kbench, profiles/r04r_sweep_nc_kbench.txt)
+  if (nrb > 128) return 1;
   for (int nc : {8, 4, 2})
     if (pad * nc <= kSweepCUs) return nc;
   return 1;

@@ -55,6 +55,9 @@ CONFIGS = {
     'c4g': (65536, 32, 16, 256, 'admm', 'uniform'),
     # strong-scaling rank of C3 at N = 8: 1024 of the 8192 samples (the per-rank step of the 8-GPU run)
     'c3s': (1024, 32, 16, 256, 'admm', 'uniform'),
+    # ... and at N = 2 and N = 4 (4096 and 2048 samples per rank)
+    'c3h': (4096, 32, 16, 256, 'admm', 'uniform'),
+    'c3q': (2048, 32, 16, 256, 'admm', 'uniform'),
 }
 CPU_BASELINE_OFF = {'c4g'}   # configs whose CPU baseline is skipped unless --cpu-baseline
 

@@ -907,7 +907,7 @@ def test_atr_fp16_split_matches_split3(shape, mods, dev, monkeypatch):
     assert out[1][3] == pytest.approx(out[0][3], rel=1e-5)
 
 
-@pytest.mark.parametrize('B', [1024, 2048, 1000, 300])
+@pytest.mark.parametrize('B', [1024, 2048, 4096, 1000, 300])
 def test_column_split_sweep_bit_identical(B, mods, dev, monkeypatch):
     """The column-split persistent sweep (k_sweep_rows NC > 1: a strong-scaling rank's few rows over
     8, 4 or 2 column groups per row block, h_t handed between the groups through memory once per t)

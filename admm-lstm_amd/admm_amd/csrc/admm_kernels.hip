@@ -438,6 +438,10 @@ __global__ __launch_bounds__(SR_THREADS) void k_sweep_rows(Geom g, const bf16x8*
   // GXC: per step parity, consumer wave and gate, the four-row sums of the tile's TW columns
   __shared__ __attribute__((aligned(16))) float Px[GXC ? 2 : 1][GXC ? 4 : 1][GXC ? 4 : 1][GXC ? TW : 1];
   __shared__ float Rg[GXC ? 5 * 256 : 1];   // GXC: the consumer threads' running range maxima
+  // the workgroup's five range maxima (float bits under LDS atomicMax): one global atomicMax per slot
+  // and workgroup at the end (sweep_done) -- with one per wave and slot, 256 workgroups queued ~5 000
+  // atomics on one cache line behind the sweep
+  __shared__ unsigned Rmax[5];
   const int T = g.T, D = g.D;
   if constexpr (NC > 1) {
     __shared__ int go_s;
@@ -470,6 +474,16 @@ __global__ __launch_bounds__(SR_THREADS) void k_sweep_rows(Geom g, const bf16x8*
     d[0] = p0; d[AP] = p1; d[2 * AP] = p2;
   };
 
+  if (threadIdx.x < 5) Rmax[threadIdx.x] = 0u;
+  auto lds_max = [&](unsigned* dst, float v) {   // wave max, one LDS atomic per wave
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, kWave));
+    if ((threadIdx.x & 63) == 0) atomicMax(dst, __float_as_uint(v));
+  };
+  auto sweep_done = [&]() {   // every wave, once, at its end
+    __syncthreads();
+    if (a.range && threadIdx.x < 5) atomicMax(reinterpret_cast<unsigned*>(a.range) + threadIdx.x, Rmax[threadIdx.x]);
+  };
   // A image for t = 1: [x_1 | h_0]
   float mh0 = 0.f;   // max |h_0| of the block's rows (range[4])
   for (int i = threadIdx.x; i < ROWS * K2; i += SR_THREADS) {
@@ -479,8 +493,8 @@ __global__ __launch_bounds__(SR_THREADS) void k_sweep_rows(Geom g, const bf16x8*
     if (k >= XK) mh0 = fmaxf(mh0, fabsf(v));
     put_a(1, row, k, v);
   }
-  if (a.range) range_max(a.range + 4, mh0);
   __syncthreads();
+  if (a.range) lds_max(&Rmax[4], mh0);
 
   if (ROWS == 16 && wave < 4) {
     // ------------------------------------------------------------------ producer, 16-row tiles
@@ -536,6 +550,7 @@ __global__ __launch_bounds__(SR_THREADS) void k_sweep_rows(Geom g, const bf16x8*
       }
     }
     __syncthreads();         // final step: the consumer drains the last tile
+    sweep_done();
     return;
   }
   if (NC > 1 && wave < 4) {
@@ -697,6 +712,7 @@ __global__ __launch_bounds__(SR_THREADS) void k_sweep_rows(Geom g, const bf16x8*
             if (d < D) out[(int64_t)d * H + 32 * (n0 + k) + 16 * h + (lane & 15)] = gx[k][h][v];
           }
     }
+    sweep_done();
     return;
   }
   if (ROWS == 32 && NC == 1 && wave < 4) {
@@ -814,6 +830,7 @@ __global__ __launch_bounds__(SR_THREADS) void k_sweep_rows(Geom g, const bf16x8*
 #ifdef SR_TIMING
     if (threadIdx.x == 0) { g_sr_wait[blockIdx.x][0] = sr_wait; g_sr_wait[blockIdx.x][1] = clock64() - sr_t0; }
 #endif
+    sweep_done();
     return;
   }
 
@@ -1115,11 +1132,11 @@ __global__ __launch_bounds__(SR_THREADS) void k_sweep_rows(Geom g, const bf16x8*
     if constexpr (GXC) {
       rq0 = Rg[ct]; rq1 = Rg[256 + ct]; rq2 = Rg[512 + ct]; rq3 = Rg[768 + ct]; rh = Rg[1024 + ct];
     }
-    range_max(a.range + 0, rq0);
-    range_max(a.range + 1, rq1);
-    range_max(a.range + 2, rq2);
-    range_max(a.range + 3, rq3);
-    range_max(a.range + 4, rh);
+    lds_max(&Rmax[0], rq0);
+    lds_max(&Rmax[1], rq1);
+    lds_max(&Rmax[2], rq2);
+    lds_max(&Rmax[3], rq3);
+    lds_max(&Rmax[4], rh);
   }
   if constexpr (GXC) {   // past the last step's barrier: its tile, then the slab (D == 1)
     const float* pp = &Px[((T - 1) * NT + NT - 1) & 1][0][cq][lane];
@@ -1132,6 +1149,7 @@ __global__ __launch_bounds__(SR_THREADS) void k_sweep_rows(Geom g, const bf16x8*
 #pragma unroll
     for (int k = 0; k < NT; ++k) out[TW * k] = gxr[k];   // slot k = column tile k after T NT + 1 turns
   }
+  sweep_done();
 #ifdef SR_TIMING
   if (threadIdx.x == 256) {
     g_sr_wait[1024 + blockIdx.x][0] = sr_wait;

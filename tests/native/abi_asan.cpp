@@ -12,6 +12,7 @@
 // Exit status 0 = every check passed and ASan reported nothing (ASan aborts on its first error).
 #include <hip/hip_runtime_api.h>
 
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -130,7 +131,9 @@ static float* zeros(size_t n) {
 
 // one context through its whole life on device 0
 static void run_context(int64_t B, int T, int D, int H, int O, int variant, int steps) {
-  std::fprintf(stderr, "context B=%lld T=%d D=%d H=%d O=%d variant=%d\n", (long long)B, T, D, H, O, variant);
+  static const auto t_start = std::chrono::steady_clock::now();
+  std::fprintf(stderr, "context B=%lld T=%d D=%d H=%d O=%d variant=%d (%.1f s)\n", (long long)B, T, D, H, O, variant,
+               std::chrono::duration<double>(std::chrono::steady_clock::now() - t_start).count());
   Lcg r{(uint32_t)(B * 131 + H)};
   std::vector<float> hx(B * T * D), hy(B * O);
   for (auto& v : hx) v = r.next();

@@ -45,7 +45,11 @@ def test_abi_argument_validation_under_asan():
 def test_abi_full_contexts_under_asan():
     if not os.path.exists(EXE):   # __graft_entry__.build() makes it best-effort
         pytest.skip('host-ASan driver not built (make -C admm-lstm_amd/admm_amd/csrc asan)')
-    r = subprocess.run([EXE, 'gpu'], env=ENV, capture_output=True, text=True, timeout=300)
+    # AddressSanitizer only: LeakSanitizer's stop-the-world check after the GPU contexts deadlocked
+    # against the ROCm runtime's threads on 2 of 4 boxes (the contexts themselves had finished in under
+    # a second); the CPU run above keeps the leak check
+    env = dict(ENV, ASAN_OPTIONS='detect_leaks=0:abort_on_error=0:halt_on_error=1')
+    r = subprocess.run([EXE, 'gpu'], env=env, capture_output=True, text=True, timeout=150)
     assert r.returncode == 0, (r.stdout + r.stderr)[-4000:]
     assert 'abi_asan gpu: ok' in r.stdout
     assert 'AddressSanitizer' not in r.stderr, r.stderr[-4000:]

@@ -172,6 +172,13 @@ int main(int argc, char** argv) {
   run_s3();
   SweepT sw{};
   sw.x = x; sw.S = S; sw.L = L; sw.zc = zc; sw.r0 = 0; sw.r1 = g.B;
+  if (getenv("KB_GX")) {   // as in the step: the next x stage's targets, G_x partials and operand ranges
+    sw.tgt = tgt;
+    sw.gx_slab = slab;
+    float* rg; (void)hipMalloc(&rg, 64); (void)hipMemset(rg, 0, 64);
+    if (!getenv("KB_NORANGE")) sw.range = rg;
+    if (getenv("KB_NOTGT")) { sw.tgt = nullptr; sw.gx_slab = nullptr; }
+  }
   timeit("sweep_t (t=5)", f4 * g.B * (g.D + 27.0 * g.H), 2.0 * g.B * (g.D + g.H) * 4 * g.H,
          [&] { launch_sweep_t(g, 5, w, hp, sw, s); });
   {

@@ -21,7 +21,7 @@ import torch  # noqa: F401  (must precede the CDLL load, see module docstring)
 LIB_PATH = os.environ.get('ADMM_LSTM_LIB') or os.path.join(os.path.dirname(os.path.abspath(__file__)),
                                                           'libadmmlstm.so')
 
-ABI_VERSION = 1
+ABI_VERSION = 2
 VARIANT_ADMM, VARIANT_NO_DUAL_Y = 0, 1
 NCCL_UNIQUE_ID_BYTES = 128
 
@@ -36,6 +36,13 @@ class NativeUnavailable(RuntimeError):
 
 class AdmmError(RuntimeError):
     """A libadmmlstm.so call returned an error code."""
+
+    def __init__(self, msg: str, code: int = 0):
+        super().__init__(msg)
+        self.code = code
+
+
+EFAULT = -6   # ADMM_EFAULT: the bound state is invalid (a column-split hand-off timed out)
 
 
 class AdmmDims(Structure):
@@ -56,7 +63,8 @@ class AdmmBuffers(Structure):
 class AdmmStats(Structure):
     _fields_ = [('steps', c_int32), ('k', c_int32 * 8), ('passes', c_int32 * 2), ('f_w', c_double * 8),
                 ('grad_sq', c_double * 8), ('theta_h', c_float), ('unresolved', c_int32), ('nonfinite', c_int32),
-                ('direct_frac', c_double * 8)]
+                ('direct_frac', c_double * 8), ('handoff_fail', c_int32), ('sweep_fallbacks', c_int32),
+                ('graph_captures', c_int32), ('graph_disabled', c_int32), ('graph_replays', c_int64)]
 
 
 # name -> (restype, argtypes)
@@ -76,6 +84,8 @@ _SIGNATURES = {
     'admm_set_comm_host': (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int]),
     'admm_get_stats': (c_int, [c_void_p, POINTER(AdmmStats)]),
     'admm_poll_status': (c_int, [c_void_p, POINTER(c_int32), POINTER(c_int32)]),
+    'admm_poll_faults': (c_int, [c_void_p, POINTER(c_int32), POINTER(c_int32)]),
+    'admm_debug_fault': (c_int, [c_void_p, c_int32]),
     'admm_profile': (c_int, [c_void_p, ctypes.c_uint32]),
     'admm_profile_read': (c_int, [c_void_p, POINTER(c_double), POINTER(c_int32)]),
     'admm_debug_workspace': (c_int, [c_void_p, c_int32, c_void_p, c_int64, c_void_p]),
@@ -121,7 +131,7 @@ def load() -> ctypes.CDLL:
 def check(rc: int, what: str) -> None:
     if rc != 0:
         msg = _lib.admm_last_error().decode(errors='replace') if _lib is not None else ''
-        raise AdmmError(f'{what} failed (code {rc}): {msg}')
+        raise AdmmError(f'{what} failed (code {rc}): {msg}', rc)
 
 
 def require_device(t: torch.Tensor, name: str) -> None:

@@ -157,10 +157,15 @@ struct AdmmCtx {
   admm_host_allreduce_fn host_ar = nullptr;
   void* host_ar_user = nullptr;
   std::vector<double> host_stage;
-  // host-mapped mirror of DevStats {unresolved, nonfinite}, written by the step's last
-  // kernel and read without a sync by admm_poll_status
+  // host-mapped mirror of DevStats {unresolved, nonfinite, handoff_fail, sweep_fallback}, written
+  // by the step's last kernel and read without a sync by admm_poll_status / admm_poll_faults
   int* status_host = nullptr;
   int* status_dev = nullptr;
+  // hand-off timeouts already reported (admm_step refuses to run on a state a timed-out hand-off
+  // left invalid until the caller rewrites it: admm_bind, admm_init_state or admm_invalidate_cache)
+  int handoff_ack = 0;
+  // admm_debug_fault: one-shot fault injection (tests)
+  bool fault_skip_publish = false, fault_capture = false;
   // optional live kernel timing (admm_profile): hipEvent pairs around launches of the
   // selected kernel classes, on the launch stream
   uint32_t prof_mask = 0;
@@ -181,6 +186,8 @@ struct AdmmCtx {
   StepSig gsig{}, last_sig{};
   bool have_last_sig = false;
   int64_t graph_replays = 0;
+  int32_t graph_captures = 0;
+  bool graph_disabled = false;   // a capture failed: steps run eagerly from then on
 };
 
 namespace {
@@ -449,7 +456,10 @@ int stage_sweep(AdmmCtx* c, hipStream_t s) {
     sa.lamh_nz = c->lamh_known && c->lamh_skip ? c->lamh_nz : nullptr;
     sa.range = c->range;   // zeroed by this step's h-stage k_reduce_g
     sa.xbuf = c->xbuf;     // zeroed by k_sweep_wt (column split only)
-    sa.fail = &c->stats->nonfinite;   // a hand-off that timed out makes the step's results invalid
+    sa.fail = &c->stats->handoff_fail;       // a hand-off that timed out makes the step's results invalid
+    sa.fallback = &c->stats->sweep_fallback;  // the column split's grid was not resident: row-block sweep ran
+    sa.skip_publish = c->fault_skip_publish ? 1 : 0;
+    c->fault_skip_publish = false;
     launch_sweep_wt(g, w, c->swt, s, c->xbuf);
     if (c->cs_poison && c->xbuf) sweep_poison_entry(g, c->xbuf, s);
     launch_sweep_rows(g, c->swt, c->hp, sa, s);
@@ -628,12 +638,12 @@ int admm_create(const AdmmDims* dims, const AdmmParams* params, int device, Admm
     admm_destroy(c);
     return fail(ADMM_EHIP, "hipMemset(stats) failed");
   }
-  if (hipHostMalloc((void**)&c->status_host, 2 * sizeof(int), hipHostMallocMapped) != hipSuccess ||
+  if (hipHostMalloc((void**)&c->status_host, 4 * sizeof(int), hipHostMallocMapped) != hipSuccess ||
       hipHostGetDevicePointer((void**)&c->status_dev, c->status_host, 0) != hipSuccess) {
     admm_destroy(c);
     return fail(ADMM_EHIP, "mapped status mirror allocation failed");
   }
-  c->status_host[0] = c->status_host[1] = 0;
+  for (int i = 0; i < 4; ++i) c->status_host[i] = 0;
   *out = c;
   return ADMM_OK;
 }
@@ -676,6 +686,7 @@ int admm_bind(AdmmCtx* c, const AdmmBuffers* b) {
     if (!b->gates[q] || !b->duals[q]) return fail(ADMM_EINVAL, "admm_bind: gate/dual %d is NULL", q);
   c->buf = *b;
   c->bound = true;
+  c->handoff_ack = c->status_host[2];
   c->z_valid = false;
   c->tgt_valid = false;
   c->gx_valid = false;
@@ -692,6 +703,7 @@ int admm_set_with_dual_y(AdmmCtx* c, int32_t flag) {
 
 int admm_invalidate_cache(AdmmCtx* c) {
   if (!c) return fail(ADMM_EINVAL, "NULL ctx");
+  c->handoff_ack = c->status_host[2];   // the caller rewrote state: a timed-out hand-off is behind it
   c->z_valid = false;
   c->tgt_valid = false;
   c->gx_valid = false;
@@ -703,6 +715,7 @@ int admm_invalidate_cache(AdmmCtx* c) {
 int admm_init_state(AdmmCtx* c, void* stream) {
   if (!c) return fail(ADMM_EINVAL, "NULL ctx");
   if (!c->bound) return fail(ADMM_ESTATE, "admm_init_state before admm_bind");
+  c->handoff_ack = c->status_host[2];
   hipStream_t s = (hipStream_t)stream;
   const Geom& g = c->g;
   DEVICE_GUARD(c->device);
@@ -792,11 +805,18 @@ void drop_graph(AdmmCtx* c) {
 int admm_step(AdmmCtx* c, void* stream) {
   if (!c) return fail(ADMM_EINVAL, "NULL ctx");
   if (!c->bound) return fail(ADMM_ESTATE, "admm_step before admm_bind");
+  {   // a column-split hand-off timed out in an earlier step (as of the last completed step): its
+      // A image held stale h, so every state since is invalid -- refuse until the caller rewrites it
+    const int hf = ((const volatile int*)c->status_host)[2];
+    if (hf > c->handoff_ack)
+      return fail(ADMM_EFAULT, "column-split sweep: %d hand-off wait(s) timed out in an earlier step; the state "
+                  "is invalid (restore it and call admm_invalidate_cache, or admm_init_state)", hf - c->handoff_ack);
+  }
   hipStream_t s = (hipStream_t)stream;
   DEVICE_GUARD(c->device);
   int rc;
   const StepSig sig = step_sig(c);
-  const bool capturable = c->graph && !c->prof_mask && !c->host_ar;
+  const bool capturable = c->graph && !c->graph_disabled && !c->prof_mask && !c->host_ar;
   if (capturable && c->gexec && sig_eq(sig, c->gsig)) {
     HIP_TRY(hipEventRecord(c->ev_gfork, s));
     HIP_TRY(hipStreamWaitEvent(c->gs, c->ev_gfork, 0));
@@ -815,22 +835,25 @@ int admm_step(AdmmCtx* c, void* stream) {
     HIP_TRY(hipStreamBeginCapture(c->gs, hipStreamCaptureModeRelaxed));
     rc = run_step(c, c->gs);
     hipError_t e = hipStreamEndCapture(c->gs, &graph);
-    if (rc) {
-      if (graph) (void)hipGraphDestroy(graph);
-      return rc;
-    }
-    if (e == hipSuccess) e = hipGraphInstantiate(&c->gexec, graph, nullptr, nullptr, 0);
+    if (e == hipSuccess && c->fault_capture) e = hipErrorUnknown;   // admm_debug_fault(2)
+    c->fault_capture = false;
+    if (rc == 0 && e == hipSuccess) e = hipGraphInstantiate(&c->gexec, graph, nullptr, nullptr, 0);
     if (graph) (void)hipGraphDestroy(graph);
-    if (e != hipSuccess) {
-      c->gexec = nullptr;
-      return fail(ADMM_EHIP, "step graph capture failed: %s", hipGetErrorString(e));
+    if (rc == 0 && e == hipSuccess) {
+      c->gsig = step_sig(c);   // == sig: the steady step leaves the flags as it found them
+      c->graph_captures++;
+      HIP_TRY(hipGraphLaunch(c->gexec, c->gs));
+      HIP_TRY(hipEventRecord(c->ev_gjoin, c->gs));
+      HIP_TRY(hipStreamWaitEvent(s, c->ev_gjoin, 0));
+      c->steps++;
+      return ADMM_OK;
     }
-    c->gsig = step_sig(c);   // == sig: the steady step leaves the flags as it found them
-    HIP_TRY(hipGraphLaunch(c->gexec, c->gs));
-    HIP_TRY(hipEventRecord(c->ev_gjoin, c->gs));
-    HIP_TRY(hipStreamWaitEvent(s, c->ev_gjoin, 0));
-    c->steps++;
-    return ADMM_OK;
+    // Nothing captured ran.  The steady step leaves the host flags as it found them (sig), so the
+    // step can run eagerly; graphs stay off for this context rather than failing every later step.
+    c->gexec = nullptr;
+    c->graph_disabled = true;
+    (void)hipGetLastError();
+    if (rc) return rc;   // the step itself failed (e.g. a collective): report that
   }
   if ((rc = run_step(c, s))) return rc;
   c->last_sig = sig;
@@ -884,7 +907,30 @@ int admm_poll_status(AdmmCtx* c, int32_t* unresolved, int32_t* nonfinite) {
   const volatile int* m = c->status_host;
   *unresolved = m[0];
   *nonfinite = m[1];
+  if (m[2] > c->handoff_ack)
+    return fail(ADMM_EFAULT, "column-split sweep: %d hand-off wait(s) timed out; the state is invalid", m[2] - c->handoff_ack);
   return ADMM_OK;
+}
+
+int admm_poll_faults(AdmmCtx* c, int32_t* handoff_fail, int32_t* sweep_fallbacks) {
+  if (!c || !handoff_fail || !sweep_fallbacks) return fail(ADMM_EINVAL, "admm_poll_faults: NULL argument");
+  const volatile int* m = c->status_host;
+  *handoff_fail = m[2];
+  *sweep_fallbacks = m[3];
+  return ADMM_OK;
+}
+
+int admm_debug_fault(AdmmCtx* c, int32_t kind) {
+  if (!c) return fail(ADMM_EINVAL, "NULL ctx");
+  switch (kind) {
+    case 0: c->fault_skip_publish = c->fault_capture = false; return ADMM_OK;
+    case 1:
+      if (!c->xbuf) return fail(ADMM_ESTATE, "admm_debug_fault(1): this context has no column-split sweep");
+      c->fault_skip_publish = true;
+      return ADMM_OK;
+    case 2: c->fault_capture = true; return ADMM_OK;
+    default: return fail(ADMM_EINVAL, "admm_debug_fault: unknown kind %d", kind);
+  }
 }
 
 int admm_profile(AdmmCtx* c, uint32_t class_mask) {
@@ -932,6 +978,11 @@ int admm_get_stats(AdmmCtx* c, AdmmStats* out) {
   out->theta_h = d.theta_h;
   out->unresolved = d.unresolved;
   out->nonfinite = d.nonfinite;
+  out->handoff_fail = d.handoff_fail;
+  out->sweep_fallbacks = d.sweep_fallback;
+  out->graph_captures = c->graph_captures;
+  out->graph_disabled = c->graph_disabled ? 1 : 0;
+  out->graph_replays = c->graph_replays;
   return ADMM_OK;
 }
 

@@ -406,6 +406,9 @@ __global__ __launch_bounds__(kThreads) void k_sweep_wt(int D, int H, int XC, Wei
 // leaves before touching the state, and the row-block sweep launched next does the work instead).
 constexpr unsigned kSweepPoison = 0x40000000u;
 constexpr uint64_t kSweepArriveTicks = 200000;   // 2 ms of the 100 MHz wall clock
+// A hand-off wait (exchange) that sees no tag t after this long gives up: 50 ms of the wall clock,
+// against ~3 us per t in a healthy sweep.  The step is then invalid and counted (SweepT::fail).
+constexpr uint64_t kHandoffTicks = 5000000;
 __device__ __forceinline__ bool sweep_arrive(unsigned* ctl, unsigned n) {
   unsigned v = __hip_atomic_fetch_add(ctl, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
   const uint64_t t0 = wall_clock64();
@@ -452,7 +455,11 @@ __global__ __launch_bounds__(SR_THREADS) void k_sweep_rows(Geom g, const bf16x8*
     __syncthreads();
     if (!go_s) return;
   } else {
-    if (a.gate && *a.gate < kSweepPoison) return;   // the column split ran
+    if (a.gate) {
+      if (*a.gate < kSweepPoison) return;   // the column split ran
+      // this launch does the sweep because the column split's grid was not resident: counted once
+      if (blockIdx.x == 0 && threadIdx.x == 0 && a.fallback) atomicAdd(a.fallback, 1);
+    }
   }
   // NC > 1: block b -> (row block rb, column group cg); the NC groups of a row block are blocks
   // b = x + 8 (NC i + cg), one XCD's under the observed round-robin placement (speed only)
@@ -908,12 +915,14 @@ __global__ __launch_bounds__(SR_THREADS) void k_sweep_rows(Geom g, const bf16x8*
     f32x4 gv[NP > 0 ? NP : 1];
     auto addr = [&](int i, int& hr, int& col) {
       const int f = ct + 256 * i;
-      hr = f / (OC / 2);
-      const int oc = 2 * (f % (OC / 2));
+      constexpr int OC2 = OC > 0 ? OC / 2 : 1;   // (NC == 1 instantiates this with OC = 0, never called)
+      hr = f / OC2;
+      const int oc = 2 * (f % OC2);
       col = oc < TW * n0 ? oc : oc + TW * NTC;
       return (t & 1) * xset + (uint32_t)(((rb * 32 + hr) * H + col) * 8);
     };
     const unsigned want = (unsigned)t;
+    uint64_t t0 = 0;
     for (unsigned spins = 0;; ++spins) {
       bool ok = true;
 #pragma unroll
@@ -924,7 +933,11 @@ __global__ __launch_bounds__(SR_THREADS) void k_sweep_rows(Geom g, const bf16x8*
 #pragma unroll
       for (int i = 0; i < NP; ++i) ok &= __float_as_uint(gv[i][1]) == want && __float_as_uint(gv[i][3]) == want;
       if (__all(ok)) break;
-      if (spins > (1u << 22)) {   // ~0.5 s: a group never published (not resident?) -- give up, flagged
+      // bounded by the wall clock (the clock is read only once a wait is not immediately served)
+      if (spins == 0) t0 = wall_clock64();
+      else if (wall_clock64() - t0 > kHandoffTicks) {
+        // a group did not publish h_t: the A image would hold stale h.  Counted per wave
+        // (DevStats::handoff_fail); the host turns it into an error (admm_step / admm_get_stats)
         if (lane == 0 && a.fail) atomicAdd(a.fail, 1);
         break;
       }
@@ -1017,7 +1030,7 @@ __global__ __launch_bounds__(SR_THREADS) void k_sweep_rows(Geom g, const bf16x8*
       // h_t first: the other groups (NC > 1) and the producer wait for it; the targets, maxima and
       // residuals below are off that path
       if constexpr (NC > 1)
-        if (!last) publish(t, n, h1);
+        if (!last && !(a.skip_publish && t == 1 && rb == 0 && cg == 1)) publish(t, n, h1);
       if (!last) {
         bf16x4 p0, p1, p2;
         split3(h1, p0, p1, p2);
@@ -3189,11 +3202,12 @@ __global__ __launch_bounds__(kThreads) void k_ht_apply(Geom g, Hyper hp, Planes6
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     stats->theta_h = th;
     stats->theta_h_own = th_own;
-    if (status) {   // host-mapped mirror for admm_poll_status (the decide kernels ran earlier on this stream)
-      __hip_atomic_store(&status[0], __hip_atomic_load(&stats->unresolved, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
-                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      __hip_atomic_store(&status[1], __hip_atomic_load(&stats->nonfinite, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
-                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (status) {   // host-mapped mirror for admm_poll_status (the decide kernels and the sweep ran earlier on this stream)
+      const int* src[4] = {&stats->unresolved, &stats->nonfinite, &stats->handoff_fail, &stats->sweep_fallback};
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        __hip_atomic_store(&status[i], __hip_atomic_load(src[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
   }
   const int64_t rs = (int64_t)g.TP() * g.H, tofs = (int64_t)g.T * g.H;

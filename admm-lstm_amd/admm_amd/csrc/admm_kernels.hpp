@@ -77,14 +77,14 @@ struct DevStats {
   int unresolved;
   int nonfinite;
   float theta_h;
-  int pad;
+  int handoff_fail;         // column-split sweep: hand-off waits that timed out (the step's state is invalid)
   double f_w[8];
   double grad_sq[8];
   double direct_frac[8];
   // admm_debug_force: the exponents (and h_T theta) the step would have taken itself
   int k_own[8];
   float theta_h_own;
-  int pad2;
+  int sweep_fallback;       // column-split sweep launches whose grid was not resident (the row-block sweep ran)
 };
 
 // ---- time step (one t): GEMM [x_t | h_{t-1}] @ [Wx; Wh] for the 4 gates + fused epilogue
@@ -112,9 +112,15 @@ struct SweepT {
   // the h-side residual so k_atr3w can scale its fp16 operands (admm_split3.hip, kRange*)
   float* range;
   // column-split sweep (sweep_rows_nc > 1): the h_t granules of every padded row block
-  // (sweep_xbuf_bytes), zeroed by launch_sweep_wt; fail (nullable) counts hand-offs that timed out
+  // (sweep_xbuf_bytes), zeroed by launch_sweep_wt; fail (nullable) counts hand-off waits that timed
+  // out (DevStats::handoff_fail: the step's results are invalid and the host raises), fallback
+  // (nullable) the launches whose grid was not all resident (DevStats::sweep_fallback)
   void* xbuf;
   int* fail;
+  int* fallback;
+  // test hook (admm_debug_fault): row block 0's column group 1 skips its publish of h_1, so that
+  // the other groups' hand-off waits time out
+  int skip_publish;
   // the row-block sweep launched after a column-split one (launch_sweep_rows): runs only if that
   // launch found its workgroups not all resident and left without touching the state (nullable)
   const unsigned* gate;

@@ -19,6 +19,7 @@
 // swapped when ((r >> 2) ^ (r >> 3)) & 1.  Fragment reads (32 consecutive rows per half-wave, one
 // half) and staging writes (8 consecutive lanes on 8 consecutive rows, one half; or 4 rows x 2
 // halves) are then conflict-free under the gfx950 bank rules (MI355X_MICROARCH.md §LDS).
+#include <cstdlib>
 #include "admm_split3.hpp"
 
 #include <type_traits>
@@ -478,12 +479,30 @@ bool split3_ok(const Geom& g) {   // 32-bit buffer offsets into the h plane and 
 
 size_t split3_gimg_floats(const Geom& g) { return (size_t)4 * g.H * g.H * 3 / 2; }
 
+// Rows accumulated in f32 (MFMA accumulators) per slab: at most atr_split_rows(g).  Each slab is
+// then summed in fp64 by k_reduce_g.  Relative error of the h-side G against fp64 on identical
+// operands (tests/test_gpu_weight_phase.py; profiles/r05b_c5_gradient_rows.txt), with the
+// reference's own form (one fp32 GEMM per t, summed in fp32) for comparison:
+//   C5 per GPU (H = 512): 16 384 rows 3.4-4.5e-6, 4 096 rows 0.7-0.9e-6 (split3 the same: it is the
+//   accumulation, not the fp16 pieces), 1 024 rows 0.5-1.4e-7; reference form 1.8-2.3e-7.
+//   C3 (H = 256): 4 096 rows 1.1-1.2e-7; reference form 1.7-2.2e-7.
+// So 4 096 rows at H = 256 and 1 024 beyond (C5: 256 slabs, +1.6 GB of slab traffic per step).
+static int64_t atr_split_rows(const Geom& g) {
+  static const long env = [] {   // ADMM_ATR_ROWS: experiment hook (tools)
+    const char* e = std::getenv("ADMM_ATR_ROWS");
+    return e ? std::atol(e) : 0L;
+  }();
+  if (env >= 256) return env;
+  return g.H <= 256 ? 4096 : 1024;
+}
 int atr3_splits(const Geom& g) {
   const int tiles = (g.H / A3_BM) * (g.H / A3_BN) * 4;
-  int ns = 256 / tiles;   // one resident wave of workgroups (one per CU)
+  int64_t ns = 256 / tiles;   // one resident wave of workgroups (one per CU) ...
+  const int64_t by_acc = (g.BT() + atr_split_rows(g) - 1) / atr_split_rows(g);
+  if (ns < by_acc) ns = by_acc;   // ... or more, so that no slab sums more than kAtrSplitRows rows
   const int64_t max_by_rows = g.BT() / 256;
-  if (ns > max_by_rows) ns = (int)max_by_rows;
-  return ns < 1 ? 1 : ns;
+  if (ns > max_by_rows) ns = max_by_rows;
+  return ns < 1 ? 1 : (int)ns;
 }
 
 void launch_atr3(const Geom& g, const float* Sh, const float* zc, const float* tgt, float* slab, int nsplit,

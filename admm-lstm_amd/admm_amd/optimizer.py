@@ -302,17 +302,24 @@ class AdmmOptimizerBase(object):
         self._poll_status()
 
     def _poll_status(self) -> None:
-        """Warn (without a device sync) when a line search ran out of its exponent window
-        or saw non-finite objective values; the counts lag by the steps still in flight."""
+        """Warn (without a device sync) when a line search ran out of its exponent window, saw
+        non-finite objective values, or the column-split sweep fell back to the row-block sweep
+        (its grid was not resident); raise ``AdmmError`` when a column-split hand-off timed out
+        (the state is invalid).  The counts lag by the steps still in flight."""
         unres, nonfin = ctypes.c_int32(), ctypes.c_int32()
+        hf, fb = ctypes.c_int32(), ctypes.c_int32()
+        N.check(self._lib.admm_poll_faults(self._ctx, ctypes.byref(hf), ctypes.byref(fb)), 'admm_poll_faults')
         N.check(self._lib.admm_poll_status(self._ctx, ctypes.byref(unres), ctypes.byref(nonfin)), 'admm_poll_status')
-        seen = getattr(self, '_status_seen', (0, 0))
+        seen = getattr(self, '_status_seen', (0, 0, 0))
         if unres.value > seen[0]:
             warning(f'{unres.value - seen[0]} weight line search(es) found no accepted exponent below 2^64 '
                     f'(admm.py:334-336 would keep doubling); theta = 2^63 was applied (last_step_stats()).')
         if nonfin.value > seen[1]:
             warning(f'{nonfin.value - seen[1]} non-finite line-search objective value(s) seen.')
-        self._status_seen = (unres.value, nonfin.value)
+        if fb.value > seen[2]:
+            warning(f'{fb.value - seen[2]} column-split sweep launch(es) could not have their whole grid resident '
+                    f'(another kernel or process on the GPU?): the row-block sweep ran instead (slower, same result).')
+        self._status_seen = (unres.value, nonfin.value, fb.value)
 
     # ------------------------------------------------------------------ extras
     def last_step_stats(self) -> dict:
@@ -329,6 +336,11 @@ class AdmmOptimizerBase(object):
             'unresolved': s.unresolved,
             'nonfinite': s.nonfinite,
             'direct_frac': {name: s.direct_frac[i] for i, name in enumerate(WEIGHT_ORDER)},
+            'handoff_fail': s.handoff_fail,
+            'sweep_fallbacks': s.sweep_fallbacks,
+            'graph_captures': s.graph_captures,
+            'graph_disabled': bool(s.graph_disabled),
+            'graph_replays': s.graph_replays,
         }
 
     # ------------------------------------------------------------------ checkpoint

@@ -181,8 +181,9 @@ def pmc_traffic(cls: str, cfg_name: str):
     if not files or cls not in CLASS_KERNELS:
         return None
     kern = json.load(open(files[-1]))['kernels']
-    # trial passes after the first return early (gates already decided): use the full pass
-    key = 'traffic_bytes_max' if cls in ('trial', 'trial_h') else 'traffic_bytes_median'
+    # trial passes after the first return early (gates already decided): use the full pass; the
+    # column-split sweep is followed by its gated row-block launch, which exits at once: the max
+    key = 'traffic_bytes_max' if cls in ('trial', 'trial_h', 'sweep') else 'traffic_bytes_median'
     for prefix in CLASS_KERNELS[cls]:     # the first kernel family present in the profile
         vals = [v[key] for k, v in kern.items() if k.startswith(prefix)]
         if vals:
@@ -194,6 +195,37 @@ def pmc_traffic(cls: str, cfg_name: str):
         T = CONFIGS[cfg_name][1]
         per *= 2 * T
     return per
+
+
+# kernel families whose MFMA-busy fraction bench.py reports (SQ pass of tools/gpu.sh mfma:<cfg>)
+MFMA_KERNELS = {'sweep': ('k_sweep_rows',), 'atr_h': ('k_atr3w<2, true>', 'k_atr3w'), 'qgemm_h': ('k_qgemm_res', 'k_qgemm3'),
+                'trial': ('k_trial_mx<true',)}
+
+
+def pmc_mfma_busy(cfg_name: str):
+    """Counted MFMA-busy fraction per kernel family from the newest committed SQ pass
+    (profiles/r*_sq_<cfg>.json, tools/gpu.sh mfma:<cfg>, tools/pmc_to_json.py --sq):
+    SQ_VALU_MFMA_BUSY_CYCLES (cycles the matrix pipe of a SIMD is busy, summed over SIMDs) over
+    4 SIMDs x SQ_BUSY_CU_CYCLES (the dispatch's busy cycles summed over CUs), i.e. the share of the
+    kernel's time the matrix cores are issuing, against gfx950's MFMA peak issue rate.  Per dispatch,
+    the largest over the family's dispatches (the gated row-block sweep launch after a column split
+    does no work).  None if there is no pass for this config."""
+    import glob
+    import json
+    files = sorted(glob.glob(os.path.join(ROOT, 'profiles', f'r*_sq_{cfg_name}.json')))
+    if not files:
+        return None
+    kern = json.load(open(files[-1]))['kernels']
+    out = {'source': os.path.relpath(files[-1], ROOT)}
+    for cls, prefixes in MFMA_KERNELS.items():
+        for prefix in prefixes:
+            vals = [v['SQ_VALU_MFMA_BUSY_CYCLES_max'] / (4.0 * v['SQ_BUSY_CU_CYCLES_max'])
+                    for k, v in kern.items() if k.startswith(prefix)
+                    and v.get('SQ_BUSY_CU_CYCLES_max') and 'SQ_VALU_MFMA_BUSY_CYCLES_max' in v]
+            if vals:
+                out[cls] = round(max(vals), 4)
+                break
+    return out
 
 
 def host_cpu():
@@ -218,54 +250,128 @@ def host_cpu():
     return model, sockets, cores
 
 
-def cpu_baseline(cfg_name: str, timed_steps: int = 3, crosscheck_threads: int = 8):
+def _read(path):
+    try:
+        with open(path) as f:
+            return f.read().strip()
+    except OSError:
+        return None
+
+
+def _cpu_list(text):
+    out = []
+    for part in (text or '').split(','):
+        if '-' in part:
+            a, b = part.split('-')
+            out.extend(range(int(a), int(b) + 1))
+        elif part.strip():
+            out.append(int(part))
+    return out
+
+
+def gpu_socket_cores(dev_index: int = 0):
+    """BASELINE.md / SURVEY.md 8(d) CPU-baseline protocol: the physical cores (one hardware thread
+    each) of the socket the GPU hangs off, among the CPUs this process may run on.  Returns
+    (cpu ids, socket id, how the socket was found)."""
+    allowed = set(os.sched_getaffinity(0)) if hasattr(os, 'sched_getaffinity') else set(range(os.cpu_count() or 1))
+    pkg_of = {c: _read(f'/sys/devices/system/cpu/cpu{c}/topology/physical_package_id') for c in allowed}
+    socket, how = None, 'socket of the lowest visible CPU (GPU NUMA node unknown)'
+    try:   # the GPU's PCI device -> its NUMA node -> that node's package
+        import torch as _t
+        pr = _t.cuda.get_device_properties(dev_index)
+        bdf = f'{pr.pci_domain_id:04x}:{pr.pci_bus_id:02x}:{pr.pci_device_id:02x}.0'
+        node = int(_read(f'/sys/bus/pci/devices/{bdf}/numa_node') or -1)
+        if node >= 0:
+            cpus = [c for c in _cpu_list(_read(f'/sys/devices/system/node/node{node}/cpulist')) if c in allowed]
+            if cpus:
+                socket = pkg_of.get(cpus[0])
+                how = f'GPU {bdf} on NUMA node {node}, package {socket}'
+    except Exception:  # pragma: no cover - older torch / no sysfs
+        pass
+    if socket is None:
+        socket = pkg_of.get(min(allowed))
+    cores, seen = [], set()
+    for c in sorted(allowed):
+        if pkg_of.get(c) != socket:
+            continue
+        sib = _cpu_list(_read(f'/sys/devices/system/cpu/cpu{c}/topology/thread_siblings_list') or str(c))
+        key = min(sib) if sib else c
+        if key in seen:
+            continue
+        seen.add(key)
+        cores.append(c)
+    return cores or sorted(allowed), socket, how
+
+
+def cgroup_cpus():
+    """The cgroup (v2) CPU quota in CPUs, or None if unlimited / unknown."""
+    q = _read('/sys/fs/cgroup/cpu.max')
+    if not q:
+        return None
+    a, _, b = q.partition(' ')
+    return None if a == 'max' else round(int(a) / int(b), 2)
+
+
+def cpu_baseline(cfg_name: str, timed_steps: int = 5, crosscheck_threads: int = 8):
     """SURVEY.md 8(d) CPU-baseline protocol on this host: the CPU oracle (a port of the reference's
-    op structure, oracle/admm_oracle.py) on the FULL batch of the config, step 1 untimed (it is
-    cheaper: zero x-side gradients), the median of steps 2..1+timed_steps on min(16, physical
-    cores per socket) threads -- the GPU's CPU share on the box -- and one more step on
-    ``crosscheck_threads`` threads to compare with the survey container's 8-thread 27.6 s/it at C3."""
+    op structure, oracle/admm_oracle.py) on the FULL batch of the config, on all physical cores of the
+    GPU-local socket, pinned in-process (os.sched_setaffinity, no re-exec), step 1 untimed (it is
+    cheaper: zero x-side gradients), the median of steps 2..1+timed_steps (2..6), and one more step on
+    ``crosscheck_threads`` of those cores to compare with the survey container's 8-thread 27.6 s/it
+    at C3 (and with the reference itself run there: tools/cpu_port_vs_ref.py)."""
     from oracle import admm_oracle as O
     from parameters import example_parameter_dictionary
     B, T, D, H, variant, gen = CONFIGS[cfg_name]
     model, sockets, per_socket = host_cpu()
+    cores, socket, how = gpu_socket_cores(0)
+    quota = cgroup_cpus()
+    old_aff = os.sched_getaffinity(0) if hasattr(os, 'sched_getaffinity') else None
+    old_threads = torch.get_num_threads()
+    threads = len(cores)
     try:
-        avail = len(os.sched_getaffinity(0))
-    except AttributeError:  # pragma: no cover
-        avail = os.cpu_count() or 1
-    threads = max(1, min(16, per_socket, avail))
-    torch.set_num_threads(threads)
-    x, y = make_data(gen, B, T, D)
-    torch.manual_seed(0)
-    W = O.init_weights(D, H, 1)
-    st = O.init_state(x, y, W)
-    stp = O.Stepper(O.Hyper.from_dict(example_parameter_dictionary['GoogleStock'], variant))
-    times = []
-    for s in range(1 + timed_steps):
-        t0 = time.time()
-        stp.step(st)
-        times.append(time.time() - t0)
-        print(f'cpu_baseline: step {s + 1} on {threads} threads: {times[-1]:.2f} s', file=sys.stderr, flush=True)
-    med = sorted(times[1:])[len(times[1:]) // 2]
-    cross = None
-    if crosscheck_threads and crosscheck_threads != threads:
-        torch.set_num_threads(crosscheck_threads)
-        t0 = time.time()
-        stp.step(st)
-        cross = time.time() - t0
-        print(f'cpu_baseline: step {2 + timed_steps} on {crosscheck_threads} threads: {cross:.2f} s',
-              file=sys.stderr, flush=True)
+        if old_aff is not None:
+            os.sched_setaffinity(0, cores)
         torch.set_num_threads(threads)
+        x, y = make_data(gen, B, T, D)
+        torch.manual_seed(0)
+        W = O.init_weights(D, H, 1)
+        st = O.init_state(x, y, W)
+        stp = O.Stepper(O.Hyper.from_dict(example_parameter_dictionary['GoogleStock'], variant))
+        times = []
+        for s in range(1 + timed_steps):
+            t0 = time.time()
+            stp.step(st)
+            times.append(time.time() - t0)
+            print(f'cpu_baseline: step {s + 1} on {threads} threads: {times[-1]:.2f} s', file=sys.stderr, flush=True)
+        med = sorted(times[1:])[len(times[1:]) // 2]
+        cross = None
+        if crosscheck_threads and crosscheck_threads < threads:
+            if old_aff is not None:
+                os.sched_setaffinity(0, cores[:crosscheck_threads])
+            torch.set_num_threads(crosscheck_threads)
+            t0 = time.time()
+            stp.step(st)
+            cross = time.time() - t0
+            print(f'cpu_baseline: step {2 + timed_steps} on {crosscheck_threads} threads: {cross:.2f} s',
+                  file=sys.stderr, flush=True)
+    finally:
+        torch.set_num_threads(old_threads)
+        if old_aff is not None:
+            os.sched_setaffinity(0, old_aff)
     return {
         'value': round(1.0 / med, 6), 'unit': 'it/s', 'cores': threads, 'kind': 'port',
         'sample': f'oracle/admm_oracle.py (reference op structure, fp32 torch CPU) on the full {cfg_name} batch '
                   f'B={B} T={T} D={D} H={H}: median of steps 2-{1 + timed_steps} = {med:.2f} s/it '
-                  f'(steps: {", ".join(f"{t:.2f}" for t in times)} s) on {threads} threads; '
+                  f'(steps: {", ".join(f"{t:.2f}" for t in times)} s) on {threads} threads pinned to the '
+                  f'physical cores of the GPU-local socket ({how}); '
                   + (f'step {2 + timed_steps} on {crosscheck_threads} threads {cross:.2f} s '
                      f'(survey container, 8 threads, reference itself: 27.6 s/it at C3); ' if cross else '')
-                  + f'host: {model}, {sockets} socket(s) x {per_socket} physical cores, {avail} CPUs visible',
+                  + f'host: {model}, {sockets} socket(s) x {per_socket} physical cores'
+                  + (f', cgroup CPU quota {quota} CPUs' if quota else ''),
         'median_step_s': round(med, 3), 'step_s': [round(t, 3) for t in times],
         'crosscheck': {'threads': crosscheck_threads, 'step_s': round(cross, 3)} if cross else None,
-        'host_cpu': {'model': model, 'sockets': sockets, 'physical_cores_per_socket': per_socket, 'visible_cpus': avail},
+        'host_cpu': {'model': model, 'sockets': sockets, 'physical_cores_per_socket': per_socket,
+                     'socket': socket, 'pinned_cpus': cores, 'cgroup_cpu_quota': quota},
     }
 
 
@@ -282,7 +388,7 @@ def main():
     # the CPU oracle runs the config's full batch: at C4g (65536 rows, 8x C3) four steps take ~15 min,
     # so it is off there unless asked for
     ap.add_argument('--cpu-baseline', action='store_true', help='time the CPU baseline even where it is off by default (c4g)')
-    ap.add_argument('--cpu-steps', type=int, default=3, help='timed CPU-baseline steps after step 1 (median)')
+    ap.add_argument('--cpu-steps', type=int, default=5, help='timed CPU-baseline steps after step 1 (median; 2..6)')
     ap.add_argument('--profile-classes', default='sweep,trial,trial_h,trial_extra,atr_x,atr_h,qgemm_x,qgemm_h,resid,small')
     # rehearsal of the N > 1 path on a one-GPU box: every rank on device 0, torch.distributed over
     # gloo, so the library stages its all-reduces through the host (not a performance number)
@@ -425,6 +531,10 @@ def main():
         roof['design_bytes'] = design_bytes
         roof['algorithmic_flops'] = flops
         roof['mfma_frac_fp32'] = flops / avg_s / PEAK_FP32_MFMA    # SURVEY.md 8(d)'s MFMA fraction
+        # the counted one (rocprofv3 SQ_VALU_MFMA_BUSY_CYCLES): matrix-pipe busy share of the kernel's time
+        busy = pmc_mfma_busy(args.config)
+        roof['mfma_busy_frac'] = busy.get(cls) if busy else None
+        roof['mfma_busy'] = busy
         roof['kernel'] = cls
         roof['avg_launch_us'] = avg_s * 1e6
         roof['launches'] = n

@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define ADMM_LSTM_ABI_VERSION 1
+#define ADMM_LSTM_ABI_VERSION 2
 
 enum {
   ADMM_OK = 0,
@@ -38,7 +38,10 @@ enum {
   ADMM_EHIP = -2,     /* HIP runtime error */
   ADMM_ENOMEM = -3,   /* device allocation failed */
   ADMM_ECOMM = -4,    /* RCCL error */
-  ADMM_ESTATE = -5    /* call not valid in the context's state (e.g. step before bind) */
+  ADMM_ESTATE = -5,   /* call not valid in the context's state (e.g. step before bind) */
+  ADMM_EFAULT = -6    /* a step's device work failed an internal check (the column-split sweep's
+                         hand-off timed out): the bound state is invalid until the caller rewrites
+                         it (admm_init_state, or a restore followed by admm_invalidate_cache) */
 };
 
 enum { ADMM_VARIANT_ADMM = 0, ADMM_VARIANT_NO_DUAL_Y = 1 };
@@ -93,6 +96,14 @@ typedef struct AdmmStats {
   int32_t nonfinite;          /* NaN/Inf seen in line-search sums (should be 0) */
   double direct_frac[8];      /* fraction of elements outside the polynomial regime of each
                                  weight search (|q| > 2^-5: per-candidate evaluation) */
+  /* ABI 2 */
+  int32_t handoff_fail;       /* column-split sweep hand-off waits that timed out, running count
+                                 (any growth invalidates the state: admm_step then fails ADMM_EFAULT) */
+  int32_t sweep_fallbacks;    /* column-split sweep launches whose grid was not all resident at once,
+                                 running count: the row-block sweep did that step's sweep (slower) */
+  int32_t graph_captures;     /* ADMM_GRAPH=1: step graphs captured */
+  int32_t graph_disabled;     /* 1 once a capture failed: steps run eagerly from then on */
+  int64_t graph_replays;      /* steps run as a replay of a captured graph */
 } AdmmStats;
 
 typedef struct AdmmCtx AdmmCtx;
@@ -152,6 +163,10 @@ int admm_get_stats(AdmmCtx* ctx, AdmmStats* out);
    non-finite objective values, as of the last step whose final kernel has completed
    (a host-mapped mirror; no device sync).  The drop-in warns when they grow. */
 int admm_poll_status(AdmmCtx* ctx, int32_t* unresolved, int32_t* nonfinite);
+/* ABI 2.  admm_poll_status also returns ADMM_EFAULT (with both counts filled) once a hand-off
+   timeout is known.  admm_poll_faults: the running counts of AdmmStats::handoff_fail and
+   ::sweep_fallbacks as of the last completed step (non-blocking, the same mirror). */
+int admm_poll_faults(AdmmCtx* ctx, int32_t* handoff_fail, int32_t* sweep_fallbacks);
 
 /* Live kernel timing (used by bench.py's roofline): when a class bit is set, admm_step
    records a hipEvent pair around every launch of that class on the step's stream.
@@ -213,6 +228,11 @@ int admm_debug_trace_resid(AdmmCtx* ctx, float* rx, float* rh);
    tests use it to follow a reference trajectory whose fp32 decisions are rounding noise
    (C1 on GoogleStock) and to arbitrate the step's own decisions along it.  k8 == NULL: off. */
 int admm_debug_force(AdmmCtx* ctx, const int32_t* k8, int32_t ht_fails);
+/* Test hook (ABI 2): one-shot fault injection into the next admm_step.  kind 1: in the column-split
+   sweep, row block 0's column group 1 skips its publish of h_1, so the other groups' hand-off waits
+   time out (ADMM_ESTATE if the context has no column split); kind 2: the next step-graph capture
+   (ADMM_GRAPH=1) fails as if hipGraphInstantiate had; 0: clear. */
+int admm_debug_fault(AdmmCtx* ctx, int32_t kind);
 int admm_debug_own(AdmmCtx* ctx, int32_t* k8_out, float* theta_h_out);
 
 /* LSTM.forward / init_gate_variables (blocks/lstm.py:43-46, 65-88) without a context.

@@ -67,6 +67,8 @@ CASES = {
     # the library runs its split-bf16 h-stage GEMMs and row-pair trials); full weights every step
     't4_pert_h256': ('admm', False, 'uniform', 1024, 8, 16, 256, 3, False, 'GoogleStock'),
     't4_pert_h512': ('no_dual_y', False, 'rw', 512, 8, 1, 512, 3, False, 'GoogleStock'),
+    # ... and at C3's own T = 32 (both line-search forms asserted at the headline's T)
+    't32_pert_h256': ('admm', False, 'uniform', 1024, 32, 16, 256, 3, False, 'GoogleStock'),
 }
 
 # compact cases: which steps keep their full weights (the others keep x2q/out in full and
@@ -77,9 +79,11 @@ COMPACT = {'c3': {'full_w': (1, 2, 3, 4, 5), 'fp64': True},
            'c5_1gpu': {'full_w': (3,), 'fp64': False},
            'c4g': {'full_w': (3,), 'fp64': False},
            't4_pert_h256': {'full_w': (1, 2, 3), 'fp64': True},
-           't4_pert_h512': {'full_w': (1, 2, 3), 'fp64': True}}
+           't4_pert_h512': {'full_w': (1, 2, 3), 'fp64': True},
+           't32_pert_h256': {'full_w': (1, 2, 3), 'fp64': True}}
 # perturbed cases: golden_io.perturb_state(seed, scale) right after the optimizer is constructed
-PERTURB = {'t4_pert_h256': {'seed': 11, 'scale': 1e-2}, 't4_pert_h512': {'seed': 11, 'scale': 1e-2}}
+PERTURB = {'t4_pert_h256': {'seed': 11, 'scale': 1e-2}, 't4_pert_h512': {'seed': 11, 'scale': 1e-2},
+           't32_pert_h256': {'seed': 11, 'scale': 1e-2}}
 WSTRIDE = 16
 
 

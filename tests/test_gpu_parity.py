@@ -936,8 +936,10 @@ def test_column_split_sweep_bit_identical(B, mods, dev, monkeypatch):
         for _ in range(4):
             opt.step()
             st = opt.last_step_stats()
-            assert st['nonfinite'] == 0 and st['unresolved'] == 0, st
+            assert st['nonfinite'] == 0 and st['unresolved'] == 0 and st['handoff_fail'] == 0, st
             ks.append(list(st['k'].values()))
+        # mode 2: every step's column split found its count poisoned and counted one fallback
+        assert st['sweep_fallbacks'] == (4 if mode == '2' else 0), st
         zc = torch.empty(4, B * T, H, device=dev)
         assert N.load().admm_debug_workspace(opt._ctx, 0, N.ptr(zc), zc.numel() * 4, N.stream_handle(dev)) == 1
         out.append((ks, torch.cat([p.detach().flatten() for p in m.parameters()]
@@ -953,10 +955,15 @@ def test_column_split_sweep_bit_identical(B, mods, dev, monkeypatch):
 @pytest.mark.parametrize('shape', [(2048, 8, 16, 256), (1024, 4, 16, 256), (300, 3, 16, 64)])
 def test_step_graph_bit_identical(shape, mods, dev, monkeypatch):
     """ADMM_GRAPH=1: once two steps start from the same launch signature, the step is captured into
-    one HIP graph and replayed.  Seven steps with an external weight write after step 4 (the caches
-    are invalidated: eager steps, then a new capture) are bitwise equal to the eager run."""
+    one HIP graph and replayed.  Eight steps with an external write to model.x2i after step 5 (a
+    tracked tensor: the caches are invalidated, the next steps run eagerly until the signature is
+    the captured one again, then replay) are bitwise equal to the eager run, and the stats count the
+    capture and replays on both sides of the write.  Mode 'fault': the first capture is made to fail
+    (admm_debug_fault(2)); that step runs eagerly, graphs stay off for the context, and the run is
+    still bitwise equal (a capture failure must not become a permanent step failure)."""
     from blocks.lstm import LSTM
     from parameters import example_parameter_dictionary
+    from admm_amd import _native as N
     admm, _ = mods
     admm.with_dual_y = False
     B, T, D, H = shape
@@ -964,24 +971,89 @@ def test_step_graph_bit_identical(shape, mods, dev, monkeypatch):
     x = torch.rand(B, T, D, generator=g).to(dev)
     y = (0.8 * x.mean((1, 2)).unsqueeze(1) + 0.1 * torch.rand(B, 1, generator=g).to(dev)).contiguous()
     out = []
-    for mode in ('0', '1'):
-        monkeypatch.setenv('ADMM_GRAPH', mode)
+    for mode in ('0', '1', 'fault'):
+        monkeypatch.setenv('ADMM_GRAPH', '0' if mode == '0' else '1')
         torch.manual_seed(0)
         m = LSTM(D, H, 1).to(dev)
         opt = admm.ADMMBasedOptimizer(m, (x, y), example_parameter_dictionary['GoogleStock'], verbose=False)
-        ks = []
-        for s_ in range(7):
+        if mode == 'fault':
+            assert N.load().admm_debug_fault(opt._ctx, 2) == 0
+        ks, rep = [], []
+        for s_ in range(8):
             opt.step()
-            ks.append(list(opt.last_step_stats()['k'].values()))
-            if s_ == 3:
+            st = opt.last_step_stats()
+            ks.append(list(st['k'].values()))
+            rep.append(st['graph_replays'])
+            if s_ == 4:
                 with torch.no_grad():
-                    m.out.mul_(1.0001)
+                    m.x2i.mul_(1.0001)
+        if mode == '1':
+            # steps 1-3 change the signature (caches and operand ranges come valid), step 4 is
+            # captured, step 5 replays; after the write two eager steps rebuild the caches, step 8
+            # replays the captured graph again
+            assert st['graph_captures'] >= 1 and not st['graph_disabled'], st
+            assert rep[4] >= 1, rep               # replayed before the write
+            assert rep[7] > rep[4], rep           # ... and again after it
+        elif mode == 'fault':
+            assert st['graph_disabled'] and st['graph_captures'] == 0 and st['graph_replays'] == 0, st
+        else:
+            assert st['graph_captures'] == 0 and st['graph_replays'] == 0, st
         out.append((ks, torch.cat([p.detach().flatten() for p in m.parameters()]
                                   + [v.flatten() for v in opt.gates.values()]
                                   + [v.flatten() for v in opt.duals.values()])))
         del opt
-    assert out[0][0] == out[1][0]
-    assert torch.equal(out[0][1], out[1][1])
+    for o in out[1:]:
+        assert out[0][0] == o[0]
+        assert torch.equal(out[0][1], o[1])
+
+
+def test_column_split_handoff_timeout_is_an_error(mods, dev):
+    """A column-split hand-off that times out must not leave stale h in the next A image silently
+    (ADVICE r4).  admm_debug_fault(1) makes row block 0's column group 1 skip its
+    publish of h_1 in the next step: the other groups' waits time out (50 ms of the wall clock),
+    the step counts it in AdmmStats::handoff_fail, admm_poll_status returns ADMM_EFAULT, and the
+    next step() raises AdmmError (code -6) instead of stepping on the invalid state.  Restoring the
+    state and invalidating the caches clears it: the step after that runs and the count stays put."""
+    from blocks.lstm import LSTM
+    from parameters import example_parameter_dictionary
+    from admm_amd import _native as N
+    admm, _ = mods
+    admm.with_dual_y = False
+    B, T, D, H = 1024, 4, 16, 256
+    g = torch.Generator().manual_seed(45)
+    x = torch.rand(B, T, D, generator=g).to(dev)
+    y = (0.8 * x.mean((1, 2)).unsqueeze(1) + 0.1 * torch.rand(B, 1, generator=g).to(dev)).contiguous()
+    torch.manual_seed(0)
+    m = LSTM(D, H, 1).to(dev)
+    opt = admm.ADMMBasedOptimizer(m, (x, y), example_parameter_dictionary['GoogleStock'], verbose=False)
+    lib = N.load()
+    opt.step()
+    assert opt.last_step_stats()['handoff_fail'] == 0
+    snap = {k: v.clone() for k, v in opt.gates.items()}, {k: v.clone() for k, v in opt.duals.items()}
+    wsnap = [p.detach().clone() for p in m.parameters()]
+    if lib.admm_debug_fault(opt._ctx, 1) != 0:
+        pytest.skip('no column-split sweep on this device (fewer than 256 CUs)')
+    opt.step()   # enqueued; the device flags the hand-off timeout
+    st = opt.last_step_stats()   # synchronises
+    assert st['handoff_fail'] > 0, st
+    unres, nonfin = ctypes.c_int32(), ctypes.c_int32()
+    assert lib.admm_poll_status(opt._ctx, ctypes.byref(unres), ctypes.byref(nonfin)) == N.EFAULT
+    with pytest.raises(N.AdmmError) as ei:
+        opt.step()
+    assert ei.value.code == N.EFAULT and 'hand-off' in str(ei.value)
+    # restore the pre-fault state (as from a checkpoint) and invalidate: stepping works again
+    with torch.no_grad():
+        for k, v in snap[0].items():
+            opt.gates[k].copy_(v)
+        for k, v in snap[1].items():
+            opt.duals[k].copy_(v)
+        for p, v in zip(m.parameters(), wsnap):
+            p.copy_(v)
+    opt.step()
+    st2 = opt.last_step_stats()
+    assert st2['handoff_fail'] == st['handoff_fail'] and st2['nonfinite'] == 0, st2
+    for p in m.parameters():
+        assert bool(torch.isfinite(p).all())
 
 
 def test_generic_weight_stage_matches_fast(mods, dev, monkeypatch):

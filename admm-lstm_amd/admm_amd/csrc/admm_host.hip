@@ -125,6 +125,9 @@ struct AdmmCtx {
   int sweep_split = 2;     // sample parts of the per-t sweep, one stream each
   bool sweep_rows = false; // whole sweep as one persistent launch (k_sweep_rows; ADMM_SWEEP_ROWS=0 disables)
   float* swt = nullptr;    // its B-operand image of the weights
+  // the image's zero padding (x rows D .. 16 XC) is written once by k_sweep_wt; after that the
+  // weight selections keep every weight element's pieces current (SelectArgs::wt)
+  bool wt_init = false;
   bool split3 = false;     // h-stage GEMMs on split bf16 MFMAs (admm_split3.hip; ADMM_SPLIT3=0 disables)
   // the h-side gradient G_h = rho Hprev^T R (k_atr3w) on split3's six products, f32-accurate
   // (tests/test_gpu_weight_phase.py: within the error of an fp32 GEMM of the same operands) ...
@@ -149,6 +152,10 @@ struct AdmmCtx {
   int wy_nsplit = 1;
   double *ht_part = nullptr, *ht_sums = nullptr;
   int ht_nblk = 1;
+  unsigned* sel_count = nullptr;  // [4] per-gate arrival counts of the fused tail selection
+  // U holds the wy residual of the bound state (written by the last step's k_ht_apply): the wy stage
+  // skips k_wy_u.  Cleared whenever the caller may have changed h_T, a, wy or the dual y flag.
+  bool u_valid = false;
   DevStats* stats = nullptr;
   // multi-GPU
   ncclComm_t comm = nullptr;
@@ -277,7 +284,7 @@ int stage_wy(AdmmCtx* c, hipStream_t s) {
   const Geom& g = c->g;
   ProfScope ps(c, ADMM_PROF_SMALL, s);
   launch_wy_grad(g, c->hp, c->buf.gates[ADMM_H], c->buf.a, c->buf.dual_y, c->buf.wy, c->U, c->wy_slab,
-                 c->wy_nsplit, s);
+                 c->wy_nsplit, s, c->u_valid);
   if (!c->comm && !c->host_ar) {   // one process: reduce and apply in one launch
     launch_wy_reduce(g, c->hp, c->wy_slab, c->wy_nsplit, c->Gy, c->buf.wy, s);
     return ADMM_OK;
@@ -356,8 +363,14 @@ int stage_weights(AdmmCtx* c, int side, hipStream_t s) {
     else if (side == 0) launch_debug_resid(g, gsrc == c->gx_slab ? 0 : 1, c->zc, c->tgt, c->trace_r[0], s);
     else launch_debug_resid(g, 2, zh, c->tgt, c->trace_r[1], s);
   }
-  launch_reduce_g(g, side, c->hp, gsrc, ns, c->G, c->found, spec && side == 0 ? c->kpred : nullptr, c->stats, s,
-                  c->p16, side == 1 ? c->range : nullptr);   // (the h side clears the ranges for the sweep)
+  // one process, split3 Q GEMM: the h side's reduce also forms the split G image for k_qgemm3 (no
+  // k_split_g launch); several processes split it after the all-reduce
+  const bool gimg_fused = side == 1 && fast && c->split3 && !c->comm && !c->host_ar;
+  if (gimg_fused)
+    launch_reduce_gh_img(g, c->hp, gsrc, ns, c->G, c->found, c->stats, s, c->p16, c->range, c->gimg);
+  else
+    launch_reduce_g(g, side, c->hp, gsrc, ns, c->G, c->found, spec && side == 0 ? c->kpred : nullptr, c->stats, s,
+                    c->p16, side == 1 ? c->range : nullptr);   // (the h side clears the ranges for the sweep)
   // (x stage with G_y pending: one all-reduce for both, then the wy update)
   const bool with_gy = side == 0 && c->gy_pending;
   int rc = allreduce_f32(c, c->G, (size_t)4 * Kd * g.H + (with_gy ? (size_t)g.H * g.O : 0), s);
@@ -372,7 +385,7 @@ int stage_weights(AdmmCtx* c, int side, hipStream_t s) {
   // 2. trial direction Q = A G (not needed on the fast x side: formed inside the trials)
   if (!(fast && side == 0)) {
     ProfScope ps(c, side == 0 ? ADMM_PROF_QGEMM_X : ADMM_PROF_QGEMM_H, s);
-    if (side == 1 && c->split3) launch_qgemm3(g, c->buf.gates[ADMM_H], c->G, c->gimg, c->Q, s);
+    if (side == 1 && c->split3) launch_qgemm3(g, c->buf.gates[ADMM_H], c->G, c->gimg, c->Q, s, gimg_fused);
     else launch_qgemm(g, side, c->buf.x, c->buf.gates[ADMM_H], c->G, c->Q, s);
   }
   // 3. line search: trial passes of kTrialJ exponents each until every gate has passed
@@ -388,6 +401,9 @@ int stage_weights(AdmmCtx* c, int side, hipStream_t s) {
   sa.pick = c->pick;
   sa.stats = c->stats;
   sa.force = c->force_on ? c->force_dev : nullptr;
+  sa.wt = c->sweep_rows ? c->swt : nullptr;   // the sweep's weight image of the updated weights
+  sa.wt_rows16 = sweep_wt_rows16(g);
+  sa.wt_xc = sweep_wt_xc(g);
   const int nblk = fast ? trial_fast_blocks(g, side) : c->nblk_trial;
   // the row-pair trial kernel (H % 256 == 0) writes one partial per (block, column block)
   const int nred = fast && side == 0 && trial_mx_ok(g) ? nblk * (g.H / 128)
@@ -399,6 +415,18 @@ int stage_weights(AdmmCtx* c, int side, hipStream_t s) {
   // (hint, k_reduce_g) that is rare, and the tail's workgroups exit at once
   for (int pass : {0, kTailPass}) {
     const int par = pass == 0 ? 0 : 1;   // parity of the found flags this pass reads
+    sa.pass = pass;
+    sa.found_in = c->found + 4 * par;
+    sa.found_out = c->found + 4 * (par ^ 1);
+    const int nwin = pass == 0 ? 1 : kMaxPasses - 1;
+    if (fused_reduce) {   // k_select reduces the partials itself (no all-reduce in between)
+      sa.part = c->tr_part;
+      sa.nred = nred;
+    } else {
+      sa.part = nullptr;
+    }
+    // one process: the tail launch makes its own selection (its last workgroup per gate)
+    const bool tail_fused = fused_reduce && fast && pass == kTailPass && tail_select_fused(g, side);
     {
       ProfScope ps(c, pass != 0 ? ADMM_PROF_TRIAL_EXTRA : side == 0 ? ADMM_PROF_TRIAL : ADMM_PROF_TRIAL_H, s);
       SpecX sx{};
@@ -411,22 +439,16 @@ int stage_weights(AdmmCtx* c, int side, hipStream_t s) {
       if (fast)
         launch_trial_fast(g, side, pass, side == 1 ? zh : c->zc, c->tgt, side == 1 ? c->Q : nullptr, c->buf.x,
                           side == 0 ? c->G : c->dW, c->found + 4 * par, c->tr_part, nblk, s, sx.zx ? &sx : nullptr,
-                          side == 1 && c->split3 ? q_layout(g) : 0);
+                          side == 1 && c->split3 ? q_layout(g) : 0, tail_fused ? &sa : nullptr,
+                          tail_fused ? &c->hp : nullptr, tail_fused ? c->sel_count : nullptr);
       else
         launch_trial(g, pass, c->zc, c->tgt, c->Q, c->found + 4 * par, c->tr_part, nblk, s);
     }
-    sa.pass = pass;
-    sa.found_in = c->found + 4 * par;
-    sa.found_out = c->found + 4 * (par ^ 1);
-    const int nwin = pass == 0 ? 1 : kMaxPasses - 1;
-    if (fused_reduce) {   // k_select reduces the partials itself (no all-reduce in between)
-      sa.part = c->tr_part;
-      sa.nred = nred;
-    } else {
+    if (tail_fused) continue;
+    if (!fused_reduce) {
       launch_trial_reduce(g, pass, c->tr_part, nred, sa.found_in, c->tr_sums, s);
       rc = allreduce_f64(c, c->tr_sums, (size_t)nwin * 4 * kTrialSlots, s);
       if (rc) return rc;
-      sa.part = nullptr;
     }
     launch_select(g, c->hp, sa, s);
   }
@@ -460,7 +482,12 @@ int stage_sweep(AdmmCtx* c, hipStream_t s) {
     sa.fallback = &c->stats->sweep_fallback;  // the column split's grid was not resident: row-block sweep ran
     sa.skip_publish = c->fault_skip_publish ? 1 : 0;
     c->fault_skip_publish = false;
-    launch_sweep_wt(g, w, c->swt, s, c->xbuf);
+    // the weight image: once (its padding); later steps' selections wrote the new weights into it,
+    // and the last step's k_ht_apply zeroed the hand-off buffer
+    if (!c->wt_init) {
+      launch_sweep_wt(g, w, c->swt, s, c->xbuf);
+      c->wt_init = true;
+    }
     if (c->cs_poison && c->xbuf) sweep_poison_entry(g, c->xbuf, s);
     launch_sweep_rows(g, c->swt, c->hp, sa, s);
   } else {
@@ -495,8 +522,9 @@ int stage_sweep(AdmmCtx* c, hipStream_t s) {
   launch_ht_reduce(c->ht_part, c->ht_nblk, c->ht_sums, s);
   int rc = allreduce_f64(c, c->ht_sums, kHTSums, s);
   if (rc) return rc;
+  // (also the next step's wy residual U: the wy stage then skips k_wy_u)
   launch_ht_apply(g, c->hp, sa.S, sa.L, c->buf.a, c->buf.dual_y, c->buf.y, c->buf.wy, c->ht_sums, c->stats,
-                  c->status_dev, s, c->force_on ? c->force_dev : nullptr);
+                  c->status_dev, s, c->force_on ? c->force_dev : nullptr, c->U, c->xbuf);
   return ADMM_OK;
 }
 
@@ -613,7 +641,7 @@ int admm_create(const AdmmDims* dims, const AdmmParams* params, int device, Admm
       (rc = dalloc(&c->found, 12)) || (rc = dalloc(&c->pick, 4)) ||
       (rc = dalloc(&c->U, (size_t)g.B * g.O)) || (rc = dalloc(&c->wy_slab, (size_t)c->wy_nsplit * g.H * g.O)) ||
       (rc = dalloc(&c->Gy, (size_t)g.H * g.O)) || (rc = dalloc(&c->ht_part, (size_t)c->ht_nblk * kHTSums)) ||
-      (rc = dalloc(&c->ht_sums, kHTSums)) || (rc = dalloc(&c->stats, 1)) || (rc = dalloc(&c->lamh_nz, 1)) || (rc = dalloc(&c->force_dev, 9)) || (rc = dalloc(&c->range, 8)) ||
+      (rc = dalloc(&c->ht_sums, kHTSums)) || (rc = dalloc(&c->sel_count, 4)) || (rc = dalloc(&c->stats, 1)) || (rc = dalloc(&c->lamh_nz, 1)) || (rc = dalloc(&c->force_dev, 9)) || (rc = dalloc(&c->range, 8)) ||
       (c->sweep_rows && (rc = dalloc(&c->swt, sweep_wt_floats(g)))) ||
       (c->sweep_rows && sweep_rows_nc(g) > 1 && cus >= kSweepCUs && (rc = dalloc(&c->xbuf, sweep_xbuf_bytes(g) / 4))) ||
       (c->split3 && (rc = dalloc(&c->gimg, split3_gimg_floats(g)))) ||
@@ -634,7 +662,8 @@ int admm_create(const AdmmDims* dims, const AdmmParams* params, int device, Admm
     admm_destroy(c);
     return fail(ADMM_EHIP, "stream/event creation failed");
   }
-  if (hipMemset(c->stats, 0, sizeof(DevStats)) != hipSuccess || hipMemset(c->range, 0, 8 * sizeof(float)) != hipSuccess) {
+  if (hipMemset(c->stats, 0, sizeof(DevStats)) != hipSuccess || hipMemset(c->range, 0, 8 * sizeof(float)) != hipSuccess ||
+      hipMemset(c->sel_count, 0, 4 * sizeof(unsigned)) != hipSuccess) {
     admm_destroy(c);
     return fail(ADMM_EHIP, "hipMemset(stats) failed");
   }
@@ -652,7 +681,7 @@ int admm_destroy(AdmmCtx* c) {
   if (!c) return ADMM_OK;
   DeviceGuard dg_(c->device);
   void* ptrs[] = {c->zc, c->tgt, c->R, c->Q, c->G, c->dW, c->gslab, c->tr_part, c->tr_sums, c->tr_poly, c->found, c->pick,
-                  c->U, c->wy_slab, c->Gy, c->ht_part, c->ht_sums, c->stats, c->swt, c->gimg, c->zx, c->kpred, c->gx_slab, c->lamh_nz, c->force_dev, c->range, c->xbuf};
+                  c->U, c->wy_slab, c->Gy, c->ht_part, c->ht_sums, c->sel_count, c->stats, c->swt, c->gimg, c->zx, c->kpred, c->gx_slab, c->lamh_nz, c->force_dev, c->range, c->xbuf};
   for (void* p : ptrs)
     if (p) (void)hipFree(p);
   if (c->comm) ncclCommDestroy(c->comm);
@@ -686,6 +715,7 @@ int admm_bind(AdmmCtx* c, const AdmmBuffers* b) {
     if (!b->gates[q] || !b->duals[q]) return fail(ADMM_EINVAL, "admm_bind: gate/dual %d is NULL", q);
   c->buf = *b;
   c->bound = true;
+  c->u_valid = false;
   c->handoff_ack = c->status_host[2];
   c->z_valid = false;
   c->tgt_valid = false;
@@ -697,6 +727,7 @@ int admm_bind(AdmmCtx* c, const AdmmBuffers* b) {
 
 int admm_set_with_dual_y(AdmmCtx* c, int32_t flag) {
   if (!c) return fail(ADMM_EINVAL, "NULL ctx");
+  if ((flag ? 1 : 0) != c->hp.with_dual_y) c->u_valid = false;   // U's dual-y shift changes
   c->hp.with_dual_y = flag ? 1 : 0;
   return ADMM_OK;
 }
@@ -704,6 +735,7 @@ int admm_set_with_dual_y(AdmmCtx* c, int32_t flag) {
 int admm_invalidate_cache(AdmmCtx* c) {
   if (!c) return fail(ADMM_EINVAL, "NULL ctx");
   c->handoff_ack = c->status_host[2];   // the caller rewrote state: a timed-out hand-off is behind it
+  c->u_valid = false;
   c->z_valid = false;
   c->tgt_valid = false;
   c->gx_valid = false;
@@ -716,6 +748,7 @@ int admm_init_state(AdmmCtx* c, void* stream) {
   if (!c) return fail(ADMM_EINVAL, "NULL ctx");
   if (!c->bound) return fail(ADMM_ESTATE, "admm_init_state before admm_bind");
   c->handoff_ack = c->status_host[2];
+  c->u_valid = false;
   hipStream_t s = (hipStream_t)stream;
   const Geom& g = c->g;
   DEVICE_GUARD(c->device);
@@ -762,7 +795,8 @@ StepSig step_sig(const AdmmCtx* c) {
   StepSig g{};
   g.flags = (c->z_valid ? 1u : 0u) | (c->tgt_valid ? 2u : 0u) | (c->gx_valid ? 4u : 0u) | (c->range_valid ? 8u : 0u) |
             (c->x1_valid ? 16u : 0u) | (c->lamh_known ? 32u : 0u) | (c->hp.with_dual_y ? 64u : 0u) |
-            (c->force_on ? 128u : 0u) | (c->prof_mask ? 256u : 0u) | (c->host_ar ? 512u : 0u);
+            (c->force_on ? 128u : 0u) | (c->prof_mask ? 256u : 0u) | (c->host_ar ? 512u : 0u) | (c->u_valid ? 1024u : 0u) |
+            (c->wt_init ? 2048u : 0u);
   g.buf = c->buf;
   g.trace[0] = c->trace_g[0]; g.trace[1] = c->trace_g[1]; g.trace[2] = c->trace_r[0]; g.trace[3] = c->trace_r[1];
   g.comm = c->comm;
@@ -786,6 +820,7 @@ int run_step(AdmmCtx* c, hipStream_t s) {
   c->tgt_valid = c->sweep_rows && fast_path(c->g) && c->tgt_sweep;
   c->gx_valid = c->tgt_valid && c->gx_slab != nullptr;
   c->range_valid = c->sweep_rows;   // the persistent sweep tracked the next weight phase's operand ranges
+  c->u_valid = true;                // k_ht_apply left the next wy stage's residual
   return ADMM_OK;
 }
 

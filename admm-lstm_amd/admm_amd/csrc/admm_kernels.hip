@@ -1130,14 +1130,18 @@ __global__ __launch_bounds__(SR_THREADS) void k_sweep_rows(Geom g, const bf16x8*
       if ((threadIdx.x & 63) == 0) { sr_comp += tb_ - ta_; sr_store += tc_ - tb_; }
 #endif
       if (NC > 1 && ct == 0) CS_STAMP(t, 2);
-      // (NC > 1: issuing these stores after the hand-off poll, so that the poll's loads do not
-      // retire behind them, measured slower: the stores then delay the mid-step barrier)
+      // (NC > 1: the hand-off comes after this tile's plane stores, although its poll loads then
+      // return behind them.  Issued after the poll but before the mid-step barrier, the stores delay
+      // the barrier (round 4); issued past it, they slow the producer's h chunks of t + 1 more than
+      // the earlier poll gains: 9.5 against 9.1 us per t at c3s, profiles/r05e_c3s_cs_phase_timing.txt)
       if (nl == NTC - 1 && !last) {
-        load_x(t + 2);       // the producer's next tile is (t+1, n0)
         if constexpr (NC > 1) exchange(t);   // the other groups' columns of h_t into this A buffer
-        SR_SYNC();           // its mid-step barrier: h_t is complete
+        SR_SYNC();           // the producer's mid-step barrier: h_t is complete
         if (NC > 1 && ct == 0) CS_STAMP(t, 6);
       }
+      // x_{t+2} into the A buffer of t+2 (the producer's z_t is done with it): needed only past the end
+      // of this step, so its loads -- each waited for by its LDS write -- stay off the mid-step path
+      if (nl == NTC - 1 && !last) load_x(t + 2);
       SR_SYNC();             // end of step
     }
   }
@@ -1499,6 +1503,61 @@ __global__ __launch_bounds__(kThreads) void k_reduce_g(int Kd, int H, int side, 
   }
   for (; sp < nsplit; ++sp) s += (double)p[(int64_t)sp * st];
   G[i] = (float)s * hp.rho[q];  // (sum_t A_t^T R_t) * rho (admm.py:312)
+}
+
+// The h stage's reduce (one process, split3 Q GEMM): k_reduce_g's G_q = rho_q sum_sp slab (the same
+// sequential fp64 sum over the splits, so the same bits) for the eight rows of one k_qgemm3 B
+// fragment per thread, which it also writes to the split G image (k_split_g's layout and split), so
+// k_split_g's launch is not needed.  gi[(((q * NK + c) * NTT + n) * 3 + p) * 64 + lane] = piece p of
+// G_q[16c + 8(lane>>5) + e][32n + (lane&31)], e = 0..7.
+__global__ __launch_bounds__(kThreads) void k_reduce_gh_img(int H, int p16, Hyper hp, const float* __restrict__ slab,
+                                                              int nsplit, float* __restrict__ G, int* found,
+                                                              const DevStats* stats, float* range_reset,
+                                                              bf16x8* __restrict__ gi) {
+  const int NK = H / 16, NTT = H / 32;
+  const int64_t per_q = (int64_t)H * H;
+  const int i = blockIdx.x * kThreads + threadIdx.x;
+  if (range_reset && i < 5) range_reset[i] = 0.f;
+  if (i < 4) {
+    found[i] = 0;
+    found[8 + i] = p16 && stats->k[2 * i + 1] >= kTrialJ ? 1 : 0;
+  }
+  if (i >= 4 * NK * NTT * 64) return;
+  const int lane = i & 63, n = (i >> 6) % NTT, c = (i / (64 * NTT)) % NK, q = i / (64 * NTT * NK);
+  const int j = 32 * n + (lane & 31), k0 = 16 * c + 8 * (lane >> 5);
+  const float* p = slab + (int64_t)q * per_q + (int64_t)k0 * H + j;
+  const int64_t st = 4 * per_q;
+  double s[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) s[e] = 0.0;
+  int sp = 0;
+  for (; sp + 4 <= nsplit; sp += 4) {   // 32 loads in flight; each element's sum in split order
+    float v[4][8];
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[u][e] = p[(int64_t)(sp + u) * st + (int64_t)e * H];
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) s[e] += (double)v[u][e];
+  }
+  for (; sp < nsplit; ++sp)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) s[e] += (double)p[(int64_t)sp * st + (int64_t)e * H];
+  float __attribute__((ext_vector_type(8))) gv;
+  float* Gq = G + (int64_t)q * per_q + (int64_t)k0 * H + j;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    gv[e] = (float)s[e] * hp.rho[q];   // as k_reduce_g (admm.py:312)
+    Gq[(int64_t)e * H] = gv[e];
+  }
+  bf16x8 p0, p1, p2;
+  split3(gv, p0, p1, p2);
+  const int base = (((q * NK + c) * NTT + n) * 3) * 64 + lane;
+  gi[base] = p0;
+  gi[base + 64] = p1;
+  gi[base + 128] = p2;
 }
 
 template <bool VEC, int SIDE>
@@ -1922,6 +1981,9 @@ __device__ __forceinline__ T wave_sum_slots(T (&v)[N]) {   // in place: v is con
   return v[0];
 }
 
+// WT: written through (sc1) and drained by the storing wave, for a reader in another workgroup of the
+// same launch (the fused tail selection, tail_select_last)
+template <bool WT = false>
 __device__ __forceinline__ void trial_block_store(float (&acc)[kSlots], double* part, int q, int blk, int nblk) {
   __shared__ double red[4][kSlots];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -1930,7 +1992,13 @@ __device__ __forceinline__ void trial_block_store(float (&acc)[kSlots], double* 
   __syncthreads();
   if (threadIdx.x < kSlots) {
     const int k = threadIdx.x;
-    part[((int64_t)q * kSlots + k) * nblk + blk] = (red[0][k] + red[1][k]) + (red[2][k] + red[3][k]);
+    const double v = (red[0][k] + red[1][k]) + (red[2][k] + red[3][k]);
+    if constexpr (WT) {
+      __hip_atomic_store(&part[((int64_t)q * kSlots + k) * nblk + blk], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else {
+      part[((int64_t)q * kSlots + k) * nblk + blk] = v;
+    }
   }
 }
 
@@ -2330,14 +2398,279 @@ __device__ __forceinline__ void trial_rows_body(const Geom& g, int q, int pass, 
 #ifndef TR_MINB
 #define TR_MINB 1   // workgroups per CU the register allocation must allow
 #endif
+// The three split pieces of the updated weight element i (row i / H of x2q or h2q, column i % H) at
+// their places in the persistent sweep's weight image (k_sweep_wt / k_sweep_wt16 layouts).
+__device__ __forceinline__ void sweep_wt_put(const SelectArgs& a, const Geom& g, int q, int64_t i, float w) {
+  const int H = g.H;
+  const int k = (int)(i / H), jj = (int)(i - (int64_t)k * H);
+  __bf16 p[3];
+  split3(w, p[0], p[1], p[2]);
+  __bf16* wt = static_cast<__bf16*>(a.wt);
+  int64_t base;
+  int e;
+  if (a.wt_rows16) {   // k_sweep_wt16: chunk 32 deep, 64-column tiles of 4 column blocks
+    const int kk = (a.side == 0 ? 0 : 32 * a.wt_xc) + k;
+    const int NT = H / 64, KC2 = a.wt_xc + H / 32;
+    const int c = kk >> 5, kq = (kk & 31) >> 3, n = jj >> 6, jq = (jj & 63) >> 4;
+    const int lane = (jj & 15) + 16 * kq;
+    base = ((((int64_t)(q * NT + n) * KC2 + c) * 4 + jq) * 3) * 64 + lane;
+    e = kk & 7;
+  } else {             // k_sweep_wt: chunk 16 deep, 32-column tiles
+    const int kk = (a.side == 0 ? 0 : 16 * a.wt_xc) + k;
+    const int NT = H / 32, KC2 = a.wt_xc + 2 * NT;
+    const int c = kk >> 4, h = (kk & 15) >> 3, n = jj >> 5;
+    const int lane = (jj & 31) + 32 * h;
+    base = (((int64_t)(q * NT + n) * KC2 + c) * 3) * 64 + lane;
+    e = kk & 7;
+  }
+#pragma unroll
+  for (int pc = 0; pc < 3; ++pc) wt[(base + 64 * pc) * 8 + e] = p[pc];
+}
+
+// k_select's work for gate q by block mb of nmb (the weight update is split over the nmb blocks).
+// LIGHT (one block of a fused tail trial launch, whose partials were handed off write-through): the
+// partials are read with sc1 loads, a few slots at a time, and ||G||^2 with fewer loads in flight --
+// the same sums in the same order, in a register budget the trial kernel can spare.
+template <bool LIGHT>
+__device__ __forceinline__ void select_gate(const Geom& g, const Hyper& hp, const SelectArgs& a, int q, int mb, int nmb) {
+  __shared__ double red[4][kSlots];
+  __shared__ double sums[kSlots];
+  __shared__ double gred[4];
+  __shared__ int pick_s;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  if (a.found_in[q]) {   // decided in an earlier pass
+    if (mb == 0 && tid == 0) {
+      a.found_out[q] = 1;
+      a.pick[q] = -1;
+    }
+    return;
+  }
+  // 2. ||G||^2 (k_decide's order: float4 loads 8 at a time)
+  const int Kd = a.side == 0 ? g.D : g.H;
+  const int64_t nW = (int64_t)Kd * g.H;
+  const float* Gq = a.G + (int64_t)q * nW;
+  double gs = 0.0;
+  if ((nW & 3) == 0) {
+    const float4* G4 = reinterpret_cast<const float4*>(Gq);
+    const int64_t n4 = nW / 4;
+    int64_t i = tid;
+    // two groups of 8 loads in flight; the sum order is the 8-at-a-time loop's
+    for (; !LIGHT && i + 15 * kThreads < n4; i += 16 * kThreads) {
+      float4 v[16];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) v[u] = G4[i + u * kThreads];
+#pragma unroll
+      for (int u = 0; u < 16; ++u)
+        gs += ((double)v[u].x * v[u].x + (double)v[u].y * v[u].y) + ((double)v[u].z * v[u].z + (double)v[u].w * v[u].w);
+    }
+    for (; i + 7 * kThreads < n4; i += 8 * kThreads) {
+      float4 v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = G4[i + u * kThreads];
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        gs += ((double)v[u].x * v[u].x + (double)v[u].y * v[u].y) + ((double)v[u].z * v[u].z + (double)v[u].w * v[u].w);
+    }
+    for (; i < n4; i += kThreads) {
+      const float4 v = G4[i];
+      gs += ((double)v.x * v.x + (double)v.y * v.y) + ((double)v.z * v.z + (double)v.w * v.w);
+    }
+  } else {
+    for (int64_t i = tid; i < nW; i += kThreads) gs += (double)Gq[i] * (double)Gq[i];
+  }
+  const double gsq = block_sum(gs, gred);
+  const float rho = hp.rho[q];
+  // per window (one, or the tail's windows 1 .. kMaxPasses - 1 in order until one decides)
+  for (int ps = pass_lo(a.pass); ps < pass_hi(a.pass); ++ps) {
+  const int64_t wofs = (int64_t)(ps - pass_lo(a.pass)) * 4 * kSlots;
+  // 1. the window's sums of this gate
+  if (a.part && LIGHT) {
+    // per slot: thread t adds partials t, t + 256, ... (k_select's order), then wave_sum (the bits of
+    // wave_sum_slots) and the same cross-wave tree
+    const double* p = a.part + wofs * a.nred + (int64_t)q * kSlots * a.nred;
+    for (int k0 = 0; k0 < kSlots; k0 += 8) {
+      double acc8[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) acc8[k] = 0.0;
+      for (int i = tid; i < a.nred; i += kThreads) {
+        double v[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+          v[k] = k0 + k < kSlots ? __hip_atomic_load(&p[(int64_t)(k0 + k) * a.nred + i], __ATOMIC_RELAXED,
+                                                     __HIP_MEMORY_SCOPE_AGENT) : 0.0;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) acc8[k] += v[k];
+      }
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const double vv = wave_sum(acc8[k]);
+        if (lane == 0 && k0 + k < kSlots) red[w][k0 + k] = vv;
+      }
+    }
+    __syncthreads();
+    if (tid < kSlots) sums[tid] = (red[0][tid] + red[1][tid]) + (red[2][tid] + red[3][tid]);
+  } else if (a.part) {
+    double acc[kSlots];
+#pragma unroll
+    for (int k = 0; k < kSlots; ++k) acc[k] = 0.0;
+    const double* p = a.part + wofs * a.nred + (int64_t)q * kSlots * a.nred;
+    int i = tid;
+    for (; i + kThreads < a.nred; i += 2 * kThreads) {   // two partials' loads in flight, same sum order
+      double v0[kSlots], v1[kSlots];
+#pragma unroll
+      for (int k = 0; k < kSlots; ++k) {
+        v0[k] = p[(int64_t)k * a.nred + i];
+        v1[k] = p[(int64_t)k * a.nred + i + kThreads];
+      }
+#pragma unroll
+      for (int k = 0; k < kSlots; ++k) acc[k] = (acc[k] + v0[k]) + v1[k];
+    }
+    if (i < a.nred) {
+#pragma unroll
+      for (int k = 0; k < kSlots; ++k) acc[k] += p[(int64_t)k * a.nred + i];
+    }
+    const double v = wave_sum_slots(acc);
+    if (lane < kSlots) red[w][lane] = v;
+    __syncthreads();
+    if (tid < kSlots) sums[tid] = (red[0][tid] + red[1][tid]) + (red[2][tid] + red[3][tid]);
+  } else if (tid < kSlots) {
+    sums[tid] = a.sums[wofs + q * kSlots + tid];
+  }
+  __syncthreads();
+  // 3. the decision
+  if (tid == 0) {
+    const double* sm = sums;
+    double* pq = a.poly + q * kPolyN;
+    double pl[kPolyN];
+    for (int n = 0; n < kPolyN; ++n) pl[n] = ps == 0 ? sm[kSlotPoly + n] : pq[n];
+    if (ps == 0 && mb == 0)
+      for (int n = 0; n < kPolyN; ++n) pq[n] = pl[n];
+    const bool poly_only = sm[kSlotNne] == 0.0;
+    const int k_lo = poly_only ? 0 : ps * kTrialJ;
+    const int k_hi = poly_only ? kMaxK : k_lo + kTrialJ;
+    int pick = -1;
+    for (int kk = k_lo; kk < k_hi; ++kk) {
+      const double sk = ldexp(1.0, -kk);
+      double poly = 0.0;
+      for (int n = kPolyN - 1; n >= 0; --n) poly = (poly + pl[n]) * sk;
+      const double cand = poly_only ? 0.0 : sm[kk - k_lo];
+      const double lhs = 0.5 * (double)rho * (cand + poly);
+      const double rhs = 0.5 * g.T * gsq * sk;
+      if (!isfinite(lhs) && mb == 0) atomicAdd(&a.stats->nonfinite, 1);
+      if (lhs > rhs) continue;
+      pick = kk;
+      break;
+    }
+    // pass 0, no exponent in the window, hint set and every per-candidate element covered by its
+    // polynomial past the window (dq_hint): decide k in [kTrialJ, kMaxK) from both polynomials
+    // (the s^1 slot only holds the per-candidate elements' linearisation, which the candidate sums
+    // needed: left out here, as the remainder has no s^1 term)
+    if (pick < 0 && ps == 0 && !poly_only && a.found_in[8 + q] && sm[kSlotN16] == 0.0) {
+      for (int kk = kTrialJ; kk < kMaxK; ++kk) {
+        const double sk = ldexp(1.0, -kk);
+        double poly = 0.0;
+        for (int n = kPolyN - 1; n >= 1; --n) poly = (poly + pl[n] + sm[kSlotP16 + n - 1]) * sk;
+        poly *= sk;
+        const double lhs = 0.5 * (double)rho * poly;
+        const double rhs = 0.5 * g.T * gsq * sk;
+        if (!isfinite(lhs) && mb == 0) atomicAdd(&a.stats->nonfinite, 1);
+        if (lhs > rhs) continue;
+        pick = kk;
+        break;
+      }
+    }
+    const int own = pick;   // -1: not decided within this pass's window
+    if (a.force) {          // test hook: take the given exponent (the search above still ran)
+      pick = a.force[2 * q + a.side];
+    } else if (pick < 0 && (poly_only || ps == kMaxPasses - 1)) {
+      pick = k_hi;
+      if (mb == 0) atomicAdd(&a.stats->unresolved, 1);
+    }
+    if (mb == 0) {
+      if (pick >= 0) {
+        const int slot = 2 * q + a.side;
+        a.stats->k[slot] = pick;
+        if (a.force) a.stats->k_own[slot] = own;
+        a.stats->f_w[slot] = 0.5 * (double)rho * sm[kSlotFw];
+        a.stats->grad_sq[slot] = gsq;
+        a.stats->direct_frac[slot] = sm[kSlotNne] / ((double)g.Bg * g.T * g.H);
+        a.stats->passes[a.side] = ps + 1;
+      }
+      a.found_out[q] = pick >= 0 ? 1 : 0;
+      a.pick[q] = pick;
+    }
+    pick_s = pick;
+  }
+  __syncthreads();
+  if (pick_s >= 0) break;
+  }
+  __syncthreads();
+  const int pick = pick_s;
+  if (pick < 0) return;
+  // 4. this block's slice of the weight update
+  const float beta = a.side == 0 ? hp.beta_x[q] : hp.beta_h[q];
+  const WUpd u = WUpd::make(rho, beta, g.T, pick);
+  float* W = a.W[q];
+  const int64_t gstride = (int64_t)nmb * kThreads;
+  int64_t i = (int64_t)mb * kThreads + tid;
+  for (; !LIGHT && i + 3 * gstride < nW; i += 4 * gstride) {   // four elements' loads in flight
+    float w0[4], gv[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) { w0[e] = W[i + e * gstride]; gv[e] = Gq[i + e * gstride]; }
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float w1 = u.apply(w0[e], gv[e]);
+      W[i + e * gstride] = w1;
+      if (a.dW) a.dW[(int64_t)q * nW + i + e * gstride] = w1 - w0[e];
+      if (a.wt) sweep_wt_put(a, g, q, i + e * gstride, w1);
+    }
+  }
+  for (; i < nW; i += gstride) {
+    const float w0 = W[i];
+    const float w1 = u.apply(w0, Gq[i]);
+    W[i] = w1;
+    if (a.dW) a.dW[(int64_t)q * nW + i] = w1 - w0;
+    if (a.wt) sweep_wt_put(a, g, q, i, w1);
+  }
+}
+
+// The tail pass's selection inside its trial launch (one process): the workgroup of gate q that
+// stores its partials last (an agent-scope count per gate; the partials went write-through, row 1
+// of MI355X_MICROARCH.md's hand-off table) runs k_select's work for q alone and re-arms the count.
+// Gates pass 0 decided: one workgroup sets their flags as k_select would (found_out 1, pick -1).
+struct TailSel {
+  SelectArgs a;
+  Hyper hp;
+  unsigned* count;   // [4], zero between launches; nullptr: not fused (a separate k_select follows)
+};
+__device__ __forceinline__ void tail_select_done(const TailSel& ts, int q) {
+  if (ts.count && blockIdx.x == 0 && blockIdx.z == 0 && threadIdx.x == 0) {
+    ts.a.found_out[q] = 1;
+    ts.a.pick[q] = -1;
+  }
+}
+__device__ __forceinline__ void tail_select_last(const Geom& g, const TailSel& ts, int q, unsigned nblocks) {
+  __shared__ int last_s;
+  __syncthreads();   // every storing wave has drained its write-through partials
+  if (threadIdx.x == 0)
+    last_s = __hip_atomic_fetch_add(&ts.count[q], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nblocks - 1;
+  __syncthreads();
+  if (!last_s) return;
+  select_gate<true>(g, ts.hp, ts.a, q, 0, 1);
+  if (threadIdx.x == 0) __hip_atomic_store(&ts.count[q], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 template <int SIDE, int DP, bool XV, bool SPEC, int QP = 0, bool TAIL = false>
 __global__ __launch_bounds__(kThreads, TR_MINB) void k_trial_rows(Geom g, int pass, const float* __restrict__ zc,
                                                          const float* __restrict__ tgt, const float* __restrict__ Q,
                                                          const float* __restrict__ x, const float* __restrict__ Gx,
                                                          const int* __restrict__ found, double* __restrict__ part,
-                                                         int nblk, SpecX sp) {
+                                                         int nblk, SpecX sp, TailSel ts) {
   const int q = blockIdx.y, blk = blockIdx.x;
-  if (found[q]) return;
+  if (found[q]) {
+    if constexpr (TAIL) tail_select_done(ts, q);
+    return;
+  }
   __shared__ float dqbuf[kThreads / 64][kDQLds];
   __shared__ float4 dwl[SPEC ? DP / 4 * 256 : 1];
   // the column blocks of one (blk, q) add into the same part slot row: blk index widened by z
@@ -2350,13 +2683,15 @@ __global__ __launch_bounds__(kThreads, TR_MINB) void k_trial_rows(Geom g, int pa
     dq_hint(dq, ps, found, q);
     if (q == 2) trial_rows_body<true, SIDE, DP, XV, SPEC, QP>(g, q, ps, zc, tgt, Q, x, Gx, blk, nblk, acc, dq, sp, dwl);
     else trial_rows_body<false, SIDE, DP, XV, SPEC, QP>(g, q, ps, zc, tgt, Q, x, Gx, blk, nblk, acc, dq, sp, dwl);
-    trial_block_store(acc, pp, q, blockIdx.z * nblk + blk, nred);
+    if (TAIL && ts.count) trial_block_store<true>(acc, pp, q, blockIdx.z * nblk + blk, nred);
+    else trial_block_store(acc, pp, q, blockIdx.z * nblk + blk, nred);
   };
   if constexpr (TAIL) {
     for (int ps = 1; ps < kMaxPasses; ++ps) {
       one(ps, part + (int64_t)(ps - 1) * 4 * kSlots * nred);
       __syncthreads();
     }
+    if (ts.count) tail_select_last(g, ts, q, (unsigned)nred);
   } else {
     one(pass, part);
   }
@@ -2488,9 +2823,12 @@ template <bool SPEC, bool TAIL = false>
 __global__ __launch_bounds__(kThreads, TMX_MINB) void k_trial_mx(Geom g, int pass, const float* __restrict__ zc,
                                                        const float* __restrict__ tgt, const float* __restrict__ x,
                                                        const float* __restrict__ Gx, const int* __restrict__ found,
-                                                       double* __restrict__ part, int nblk, SpecX sp) {
+                                                       double* __restrict__ part, int nblk, SpecX sp, TailSel ts) {
   const int q = blockIdx.y, blk = blockIdx.x;
-  if (found[q]) return;
+  if (found[q]) {
+    if constexpr (TAIL) tail_select_done(ts, q);
+    return;
+  }
   __shared__ float dqbuf[kThreads / 64][kDQLds];
   const int nred = nblk * gridDim.z;
   auto one = [&](int ps, double* pp) {
@@ -2501,13 +2839,15 @@ __global__ __launch_bounds__(kThreads, TMX_MINB) void k_trial_mx(Geom g, int pas
     dq_hint(dq, ps, found, q);
     if (q == 2) trial_mx_body<true, SPEC>(g, q, ps, zc, tgt, x, Gx, blk, nblk, acc, dq, sp);
     else trial_mx_body<false, SPEC>(g, q, ps, zc, tgt, x, Gx, blk, nblk, acc, dq, sp);
-    trial_block_store(acc, pp, q, blockIdx.z * nblk + blk, nred);
+    if (TAIL && ts.count) trial_block_store<true>(acc, pp, q, blockIdx.z * nblk + blk, nred);
+    else trial_block_store(acc, pp, q, blockIdx.z * nblk + blk, nred);
   };
   if constexpr (TAIL) {
     for (int ps = 1; ps < kMaxPasses; ++ps) {
       one(ps, part + (int64_t)(ps - 1) * 4 * kSlots * nred);
       __syncthreads();
     }
+    if (ts.count) tail_select_last(g, ts, q, (unsigned)nred);
   } else {
     one(pass, part);
   }
@@ -2745,178 +3085,7 @@ __global__ __launch_bounds__(kThreads) void k_trial_reduce(int pass, const doubl
 constexpr int kSelBlocks = 16;
 
 __global__ __launch_bounds__(kThreads) void k_select(Geom g, Hyper hp, SelectArgs a) {
-  __shared__ double red[4][kSlots];
-  __shared__ double sums[kSlots];
-  __shared__ double gred[4];
-  __shared__ int pick_s;
-  const int q = blockIdx.y, mb = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  if (a.found_in[q]) {   // decided in an earlier pass
-    if (mb == 0 && tid == 0) {
-      a.found_out[q] = 1;
-      a.pick[q] = -1;
-    }
-    return;
-  }
-  // 2. ||G||^2 (k_decide's order: float4 loads 8 at a time)
-  const int Kd = a.side == 0 ? g.D : g.H;
-  const int64_t nW = (int64_t)Kd * g.H;
-  const float* Gq = a.G + (int64_t)q * nW;
-  double gs = 0.0;
-  if ((nW & 3) == 0) {
-    const float4* G4 = reinterpret_cast<const float4*>(Gq);
-    const int64_t n4 = nW / 4;
-    int64_t i = tid;
-    // two groups of 8 loads in flight; the sum order is the 8-at-a-time loop's
-    for (; i + 15 * kThreads < n4; i += 16 * kThreads) {
-      float4 v[16];
-#pragma unroll
-      for (int u = 0; u < 16; ++u) v[u] = G4[i + u * kThreads];
-#pragma unroll
-      for (int u = 0; u < 16; ++u)
-        gs += ((double)v[u].x * v[u].x + (double)v[u].y * v[u].y) + ((double)v[u].z * v[u].z + (double)v[u].w * v[u].w);
-    }
-    for (; i + 7 * kThreads < n4; i += 8 * kThreads) {
-      float4 v[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) v[u] = G4[i + u * kThreads];
-#pragma unroll
-      for (int u = 0; u < 8; ++u)
-        gs += ((double)v[u].x * v[u].x + (double)v[u].y * v[u].y) + ((double)v[u].z * v[u].z + (double)v[u].w * v[u].w);
-    }
-    for (; i < n4; i += kThreads) {
-      const float4 v = G4[i];
-      gs += ((double)v.x * v.x + (double)v.y * v.y) + ((double)v.z * v.z + (double)v.w * v.w);
-    }
-  } else {
-    for (int64_t i = tid; i < nW; i += kThreads) gs += (double)Gq[i] * (double)Gq[i];
-  }
-  const double gsq = block_sum(gs, gred);
-  const float rho = hp.rho[q];
-  // per window (one, or the tail's windows 1 .. kMaxPasses - 1 in order until one decides)
-  for (int ps = pass_lo(a.pass); ps < pass_hi(a.pass); ++ps) {
-  const int64_t wofs = (int64_t)(ps - pass_lo(a.pass)) * 4 * kSlots;
-  // 1. the window's sums of this gate
-  if (a.part) {
-    double acc[kSlots];
-#pragma unroll
-    for (int k = 0; k < kSlots; ++k) acc[k] = 0.0;
-    const double* p = a.part + wofs * a.nred + (int64_t)q * kSlots * a.nred;
-    int i = tid;
-    for (; i + kThreads < a.nred; i += 2 * kThreads) {   // two partials' loads in flight, same sum order
-      double v0[kSlots], v1[kSlots];
-#pragma unroll
-      for (int k = 0; k < kSlots; ++k) {
-        v0[k] = p[(int64_t)k * a.nred + i];
-        v1[k] = p[(int64_t)k * a.nred + i + kThreads];
-      }
-#pragma unroll
-      for (int k = 0; k < kSlots; ++k) acc[k] = (acc[k] + v0[k]) + v1[k];
-    }
-    if (i < a.nred) {
-#pragma unroll
-      for (int k = 0; k < kSlots; ++k) acc[k] += p[(int64_t)k * a.nred + i];
-    }
-    const double v = wave_sum_slots(acc);
-    if (lane < kSlots) red[w][lane] = v;
-    __syncthreads();
-    if (tid < kSlots) sums[tid] = (red[0][tid] + red[1][tid]) + (red[2][tid] + red[3][tid]);
-  } else if (tid < kSlots) {
-    sums[tid] = a.sums[wofs + q * kSlots + tid];
-  }
-  __syncthreads();
-  // 3. the decision
-  if (tid == 0) {
-    const double* sm = sums;
-    double* pq = a.poly + q * kPolyN;
-    double pl[kPolyN];
-    for (int n = 0; n < kPolyN; ++n) pl[n] = ps == 0 ? sm[kSlotPoly + n] : pq[n];
-    if (ps == 0 && mb == 0)
-      for (int n = 0; n < kPolyN; ++n) pq[n] = pl[n];
-    const bool poly_only = sm[kSlotNne] == 0.0;
-    const int k_lo = poly_only ? 0 : ps * kTrialJ;
-    const int k_hi = poly_only ? kMaxK : k_lo + kTrialJ;
-    int pick = -1;
-    for (int kk = k_lo; kk < k_hi; ++kk) {
-      const double sk = ldexp(1.0, -kk);
-      double poly = 0.0;
-      for (int n = kPolyN - 1; n >= 0; --n) poly = (poly + pl[n]) * sk;
-      const double cand = poly_only ? 0.0 : sm[kk - k_lo];
-      const double lhs = 0.5 * (double)rho * (cand + poly);
-      const double rhs = 0.5 * g.T * gsq * sk;
-      if (!isfinite(lhs) && mb == 0) atomicAdd(&a.stats->nonfinite, 1);
-      if (lhs > rhs) continue;
-      pick = kk;
-      break;
-    }
-    // pass 0, no exponent in the window, hint set and every per-candidate element covered by its
-    // polynomial past the window (dq_hint): decide k in [kTrialJ, kMaxK) from both polynomials
-    // (the s^1 slot only holds the per-candidate elements' linearisation, which the candidate sums
-    // needed: left out here, as the remainder has no s^1 term)
-    if (pick < 0 && ps == 0 && !poly_only && a.found_in[8 + q] && sm[kSlotN16] == 0.0) {
-      for (int kk = kTrialJ; kk < kMaxK; ++kk) {
-        const double sk = ldexp(1.0, -kk);
-        double poly = 0.0;
-        for (int n = kPolyN - 1; n >= 1; --n) poly = (poly + pl[n] + sm[kSlotP16 + n - 1]) * sk;
-        poly *= sk;
-        const double lhs = 0.5 * (double)rho * poly;
-        const double rhs = 0.5 * g.T * gsq * sk;
-        if (!isfinite(lhs) && mb == 0) atomicAdd(&a.stats->nonfinite, 1);
-        if (lhs > rhs) continue;
-        pick = kk;
-        break;
-      }
-    }
-    const int own = pick;   // -1: not decided within this pass's window
-    if (a.force) {          // test hook: take the given exponent (the search above still ran)
-      pick = a.force[2 * q + a.side];
-    } else if (pick < 0 && (poly_only || ps == kMaxPasses - 1)) {
-      pick = k_hi;
-      if (mb == 0) atomicAdd(&a.stats->unresolved, 1);
-    }
-    if (mb == 0) {
-      if (pick >= 0) {
-        const int slot = 2 * q + a.side;
-        a.stats->k[slot] = pick;
-        if (a.force) a.stats->k_own[slot] = own;
-        a.stats->f_w[slot] = 0.5 * (double)rho * sm[kSlotFw];
-        a.stats->grad_sq[slot] = gsq;
-        a.stats->direct_frac[slot] = sm[kSlotNne] / ((double)g.Bg * g.T * g.H);
-        a.stats->passes[a.side] = ps + 1;
-      }
-      a.found_out[q] = pick >= 0 ? 1 : 0;
-      a.pick[q] = pick;
-    }
-    pick_s = pick;
-  }
-  __syncthreads();
-  if (pick_s >= 0) break;
-  }
-  __syncthreads();
-  const int pick = pick_s;
-  if (pick < 0) return;
-  // 4. this block's slice of the weight update
-  const float beta = a.side == 0 ? hp.beta_x[q] : hp.beta_h[q];
-  const WUpd u = WUpd::make(rho, beta, g.T, pick);
-  float* W = a.W[q];
-  const int64_t gstride = (int64_t)gridDim.x * kThreads;
-  int64_t i = (int64_t)mb * kThreads + tid;
-  for (; i + 3 * gstride < nW; i += 4 * gstride) {   // four elements' loads in flight
-    float w0[4], gv[4];
-#pragma unroll
-    for (int e = 0; e < 4; ++e) { w0[e] = W[i + e * gstride]; gv[e] = Gq[i + e * gstride]; }
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const float w1 = u.apply(w0[e], gv[e]);
-      W[i + e * gstride] = w1;
-      if (a.dW) a.dW[(int64_t)q * nW + i + e * gstride] = w1 - w0[e];
-    }
-  }
-  for (; i < nW; i += gstride) {
-    const float w0 = W[i];
-    const float w1 = u.apply(w0, Gq[i]);
-    W[i] = w1;
-    if (a.dW) a.dW[(int64_t)q * nW + i] = w1 - w0;
-  }
+  select_gate<false>(g, hp, a, blockIdx.y, blockIdx.x, gridDim.x);
 }
 
 // ============================================================================ wy
@@ -3063,6 +3232,33 @@ __device__ __forceinline__ float ht_grad(const Geom& g, const Hyper& hp, const H
   return hp.rho[5] * s;
 }
 
+// The h_T search's kHTSums sums of nblk per-block partials: thread t adds partials t, t + 256, ...
+// per sum, then the fixed wave / cross-wave tree.  (Folding this into k_ht_partial's last-arriving
+// workgroup -- write-through partials, an arrival count -- measured slower than the launch: 18.0 against
+// 10.6 + 4.7 us at c3s, profiles/r05f_c3s_step_timeline.txt.)
+__device__ __forceinline__ void ht_reduce_block(const double* part, int nblk, double* sums) {
+  __shared__ double red[4][kHTSums];
+  double s[kHTSums];
+#pragma unroll
+  for (int i = 0; i < kHTSums; ++i) s[i] = 0.0;
+  for (int b = threadIdx.x; b < nblk; b += kThreads) {
+#pragma unroll
+    for (int i = 0; i < kHTSums; ++i)
+      s[i] += part[(int64_t)b * kHTSums + i];
+  }
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+  for (int i = 0; i < kHTSums; ++i) {
+    const double v = wave_sum(s[i]);
+    if (lane == 0) red[w][i] = v;
+  }
+  __syncthreads();
+  if (threadIdx.x < kHTSums) {
+    const int i = threadIdx.x;
+    sums[i] = (red[0][i] + red[1][i]) + (red[2][i] + red[3][i]);
+  }
+}
+
 // OC > 0: compile-time output count; OC == 0: runtime g.O, 4 * g.O floats of dynamic LDS
 template <int OC>
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(8))) void k_ht_partial(Geom g, Hyper hp, Planes6 S, Planes6 L, const float* a,
@@ -3147,25 +3343,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(8))) v
 // all kHTSums sums in one pass over the partials (per sum: thread t adds partials t, t + 256, ...,
 // then block_sum's fixed tree -- the order of a per-sum loop, one barrier instead of 2 kHTSums)
 __global__ __launch_bounds__(kThreads) void k_ht_reduce(const double* part, int nblk, double* sums) {
-  __shared__ double red[4][kHTSums];
-  double s[kHTSums];
-#pragma unroll
-  for (int i = 0; i < kHTSums; ++i) s[i] = 0.0;
-  for (int b = threadIdx.x; b < nblk; b += kThreads) {
-#pragma unroll
-    for (int i = 0; i < kHTSums; ++i) s[i] += part[(int64_t)b * kHTSums + i];
-  }
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-#pragma unroll
-  for (int i = 0; i < kHTSums; ++i) {
-    const double v = wave_sum(s[i]);
-    if (lane == 0) red[w][i] = v;
-  }
-  __syncthreads();
-  if (threadIdx.x < kHTSums) {
-    const int i = threadIdx.x;
-    sums[i] = (red[0][i] + red[1][i]) + (red[2][i] + red[3][i]);
-  }
+  ht_reduce_block(part, nblk, sums);
 }
 
 __device__ __forceinline__ float ht_theta_star(const Hyper& hp, const double* sums) {
@@ -3187,7 +3365,10 @@ __device__ __forceinline__ float ht_theta_star(const Hyper& hp, const double* su
 template <int OC>
 __global__ __launch_bounds__(kThreads) void k_ht_apply(Geom g, Hyper hp, Planes6 S, Planes6 L, float* a, float* Ly,
                                                          const float* y, const float* wy, const double* sums,
-                                                         DevStats* stats, int* status, const int* force) {
+                                                         DevStats* stats, int* status, const int* force, float* U,
+                                                         uint4* __restrict__ xbuf, int nx) {
+  // the next step's column-split sweep starts from zeroed hand-off granules and entry count
+  for (int i = blockIdx.x * kThreads + threadIdx.x; i < nx; i += gridDim.x * kThreads) xbuf[i] = make_uint4(0u, 0u, 0u, 0u);
   constexpr int CW = OC > 0 ? OC : kOChunk;
   const int NO = OC > 0 ? OC : g.O;
   extern __shared__ float ht_u[];
@@ -3250,7 +3431,15 @@ __global__ __launch_bounds__(kThreads) void k_ht_apply(Geom g, Hyper hp, Planes6
             an = (Bry * hwo + 2.f * y[i]) / (2.f + Bry);
           }
           a[i] = an;
-          if (shift) Ly[i] = Ly[i] + ry * (an - hwo);
+          float ly_new = 0.f;
+          if (shift) Ly[i] = ly_new = Ly[i] + ry * (an - hwo);
+          // U (nullable): the next step's wy residual rho_y (h_T wy - a - s) of this row, which k_wy_u
+          // would form from the same h_T, wy, a and dual y (hwo is its h_T . wy, same order)
+          if (U) {
+            float u = hwo - an;
+            if (shift) u = u - ly_new / ry;
+            U[i] = ry * u;
+          }
         }
       }
     }
@@ -3350,6 +3539,8 @@ void sweep_poison_entry(const Geom& g, void* xbuf, hipStream_t s) {
 size_t sweep_xbuf_bytes(const Geom& g) { return (size_t)sweep_row_blocks_padded(g) * 32 * g.H * 8 * 2 + 256; }
 
 static int sweep_xc(const Geom& g) { return sweep_r16(g) ? (g.D + 31) / 32 : (g.D + 15) / 16; }
+int sweep_wt_rows16(const Geom& g) { return sweep_r16(g) ? 1 : 0; }
+int sweep_wt_xc(const Geom& g) { return sweep_xc(g); }
 
 size_t sweep_wt_floats(const Geom& g) {   // bf16x8 image, in float units
   if (sweep_r16(g)) return (size_t)4 * (g.H / 64) * (sweep_xc(g) + g.H / 32) * 4 * 3 * 64 * 4;
@@ -3479,6 +3670,13 @@ void launch_reduce_g(const Geom& g, int side, const Hyper& hp, const float* slab
   const int64_t n = 4LL * Kd * g.H;
   k_reduce_g<<<cdiv64(n, kThreads), kThreads, 0, s>>>(Kd, g.H, side, p16 ? 1 : 0, hp, slab, nsplit, G, found, kpred,
                                                        stats, range_reset);
+}
+
+void launch_reduce_gh_img(const Geom& g, const Hyper& hp, const float* slab, int nsplit, float* G, int* found,
+                          const DevStats* stats, hipStream_t s, bool p16, float* range_reset, float* gimg) {
+  const int total = 4 * (g.H / 16) * (g.H / 32) * 64;
+  k_reduce_gh_img<<<cdiv64(total, kThreads), kThreads, 0, s>>>(g.H, p16 ? 1 : 0, hp, slab, nsplit, G, found, stats,
+                                                               range_reset, reinterpret_cast<bf16x8*>(gimg));
 }
 
 void launch_qgemm(const Geom& g, int side, const float* x, const float* Sh, const float* G, float* Q,
@@ -3625,6 +3823,10 @@ int trial_fast_blocks(const Geom& g, int side) {
   return sb;
 }
 
+bool tail_select_fused(const Geom& g, int side) {
+  return side == 1 ? trial_rows_ok(g) : trial_mx_ok(g);
+}
+
 bool trial_mx_ok(const Geom& g) {   // else (a gate plane past 2 GB) the x side runs on k_trial_rows (VALU q)
   // 32-bit buffer offsets within one gate plane
   return g.H % 256 == 0 && g.D <= 16 && g.BT() * g.H * 4 < (int64_t)INT32_MAX;
@@ -3632,18 +3834,24 @@ bool trial_mx_ok(const Geom& g) {   // else (a gate plane past 2 GB) the x side 
 
 void launch_trial_fast(const Geom& g, int side, int pass, const float* zc, const float* tgt, const float* Q,
                        const float* x, const float* Wsrc, const int* found, double* part, int nblk, hipStream_t s,
-                       const SpecX* spec, int qpair) {
+                       const SpecX* spec, int qpair, const SelectArgs* fsel, const Hyper* fhp, unsigned* fcount) {
   dim3 grid(nblk, 4);
   const SpecX sp = spec ? *spec : SpecX{};
+  TailSel ts{};
+  if (pass == kTailPass && fsel && fhp && fcount && tail_select_fused(g, side)) {
+    ts.a = *fsel;
+    ts.hp = *fhp;
+    ts.count = fcount;
+  }
   // TAIL: the windows 1 .. kMaxPasses - 1 in one launch (pass == kTailPass); only pass 0 speculates
   auto go = [&](auto tail) {
     constexpr bool TL = decltype(tail)::value;
     if (side == 1 && trial_rows_ok(g)) {
       dim3 gr(nblk, 4, g.H / 256);
       if (qpair == 2 && qpair_ok(g))
-        k_trial_rows<1, 4, false, false, 2, TL><<<gr, kThreads, 0, s>>>(g, pass, zc, tgt, Q, x, Wsrc, found, part, nblk, sp);
+        k_trial_rows<1, 4, false, false, 2, TL><<<gr, kThreads, 0, s>>>(g, pass, zc, tgt, Q, x, Wsrc, found, part, nblk, sp, ts);
       else
-        k_trial_rows<1, 4, false, false, 0, TL><<<gr, kThreads, 0, s>>>(g, pass, zc, tgt, Q, x, Wsrc, found, part, nblk, sp);
+        k_trial_rows<1, 4, false, false, 0, TL><<<gr, kThreads, 0, s>>>(g, pass, zc, tgt, Q, x, Wsrc, found, part, nblk, sp, ts);
       return;
     }
     if (side == 1) {  // no x . W product on this side: one instantiation
@@ -3652,8 +3860,8 @@ void launch_trial_fast(const Geom& g, int side, int pass, const float* zc, const
     }
     if (trial_mx_ok(g)) {   // side 0 on the matrix cores
       dim3 gr(nblk, 4, g.H / 128);
-      if (spec && !TL) k_trial_mx<true, false><<<gr, kThreads, 0, s>>>(g, pass, zc, tgt, x, Wsrc, found, part, nblk, sp);
-      else k_trial_mx<false, TL><<<gr, kThreads, 0, s>>>(g, pass, zc, tgt, x, Wsrc, found, part, nblk, sp);
+      if (spec && !TL) k_trial_mx<true, false><<<gr, kThreads, 0, s>>>(g, pass, zc, tgt, x, Wsrc, found, part, nblk, sp, ts);
+      else k_trial_mx<false, TL><<<gr, kThreads, 0, s>>>(g, pass, zc, tgt, x, Wsrc, found, part, nblk, sp, ts);
       return;
     }
     if (trial_rows_ok(g)) {
@@ -3661,10 +3869,10 @@ void launch_trial_fast(const Geom& g, int side, int pass, const float* zc, const
       with_dp(g, [&](auto dp, auto xv) {
         if (spec && !TL)
           k_trial_rows<0, decltype(dp)::value, decltype(xv)::value, true, 0, false>
-              <<<gr, kThreads, 0, s>>>(g, pass, zc, tgt, Q, x, Wsrc, found, part, nblk, sp);
+              <<<gr, kThreads, 0, s>>>(g, pass, zc, tgt, Q, x, Wsrc, found, part, nblk, sp, TailSel{});
         else
           k_trial_rows<0, decltype(dp)::value, decltype(xv)::value, false, 0, TL>
-              <<<gr, kThreads, 0, s>>>(g, pass, zc, tgt, Q, x, Wsrc, found, part, nblk, sp);
+              <<<gr, kThreads, 0, s>>>(g, pass, zc, tgt, Q, x, Wsrc, found, part, nblk, sp, TailSel{});
       });
       return;
     }
@@ -3692,10 +3900,10 @@ int wy_splits(const Geom& g) {   // 64 rows per split: the strided h_T loads are
 }
 
 void launch_wy_grad(const Geom& g, const Hyper& hp, const float* Sh, const float* a, const float* Ly,
-                    const float* wy, float* U, float* slab, int nsplit, hipStream_t s) {
+                    const float* wy, float* U, float* slab, int nsplit, hipStream_t s, bool u_ready) {
   int nb = cdiv64(g.B, 4);
   if (nb > 2048) nb = 2048;
-  k_wy_u<<<nb, kThreads, 0, s>>>(g, hp, Sh, a, Ly, wy, U);
+  if (!u_ready) k_wy_u<<<nb, kThreads, 0, s>>>(g, hp, Sh, a, Ly, wy, U);
   const int64_t nHO = (int64_t)g.H * g.O;
   dim3 grid(cdiv64(nHO, kThreads), nsplit);
   k_wy_slab<<<grid, kThreads, 0, s>>>(g, Sh, U, slab, nsplit);
@@ -3735,10 +3943,12 @@ void launch_ht_reduce(const double* part, int nblk, double* sums, hipStream_t s)
 
 void launch_ht_apply(const Geom& g, const Hyper& hp, const Planes6& S, const Planes6& L, float* a, float* Ly,
                      const float* y, const float* wy, const double* sums, DevStats* stats, int* status, hipStream_t s,
-                     const int* force) {
-  if (g.O == 1) k_ht_apply<1><<<ht_blocks(g), kThreads, 0, s>>>(g, hp, S, L, a, Ly, y, wy, sums, stats, status, force);
+                     const int* force, float* U, void* xbuf) {
+  const int nx = xbuf ? (int)(sweep_xbuf_bytes(g) / 16) : 0;
+  uint4* xb = static_cast<uint4*>(xbuf);
+  if (g.O == 1) k_ht_apply<1><<<ht_blocks(g), kThreads, 0, s>>>(g, hp, S, L, a, Ly, y, wy, sums, stats, status, force, U, xb, nx);
   else k_ht_apply<0><<<ht_blocks(g), kThreads, 4 * g.O * sizeof(float), s>>>(g, hp, S, L, a, Ly, y, wy, sums, stats,
-                                                                            status, force);
+                                                                            status, force, U, xb, nx);
 }
 
 #ifdef SR_CS_TIMING

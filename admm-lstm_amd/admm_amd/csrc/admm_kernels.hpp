@@ -145,6 +145,8 @@ int sweep_row_blocks_padded(const Geom& g);
 size_t sweep_xbuf_bytes(const Geom& g);
 // xbuf (nullable): zeroed in the same launch (before a column-split sweep)
 void launch_sweep_wt(const Geom& g, const Weights& w, float* wt, hipStream_t s, void* xbuf = nullptr);
+int sweep_wt_rows16(const Geom& g);   // the image layout of launch_sweep_wt: 1 = 16-row tiles
+int sweep_wt_xc(const Geom& g);       // its x chunks
 void launch_sweep_rows(const Geom& g, const float* wt, const Hyper& hp, const SweepT& a, hipStream_t s);
 // flag |= 1 if lh[b][t][j] != 0 for some t in [1, T) (H % 4 == 0; flag zeroed by the caller)
 void launch_check_lamh(const Geom& g, const float* lh, int* flag, hipStream_t s);
@@ -181,6 +183,10 @@ void launch_reduce_g(const Geom& g, int side, const Hyper& hp, const float* Gsla
                      int* kpred, const DevStats* stats,
                      hipStream_t s,
                      bool p16 = true, float* range_reset = nullptr);   // range_reset: zero range[0..4] (SweepT::range)
+// h side, one process, split3 Q GEMM: launch_reduce_g's G (bitwise the same) and, in the same launch,
+// the split G image that launch_qgemm3 would form (gimg: split3_gimg_floats(g); H % 32 == 0)
+void launch_reduce_gh_img(const Geom& g, const Hyper& hp, const float* slab, int nsplit, float* G, int* found,
+                          const DevStats* stats, hipStream_t s, bool p16, float* range_reset, float* gimg);
 // Q[q][row][j] = sum_m A[row][m] * G[q][m][j]
 void launch_qgemm(const Geom& g, int side, const float* x, const float* Sh, const float* G, float* Q,
                   hipStream_t s);
@@ -218,9 +224,15 @@ struct SpecX {
   float* zx;                // [4][BT][H] z of the h stage (zc + x dWx)
   Hyper hp;
 };
+// fsel, fhp, fcount (one process, pass == kTailPass, tail_select_fused): the tail launch also makes
+// the tail's selection (k_select's work, by the last workgroup of each gate; fcount: [4] zeroed
+// counters the kernel re-arms), so no launch_select follows it
+struct SelectArgs;
 void launch_trial_fast(const Geom& g, int side, int pass, const float* zc, const float* tgt, const float* Q,
                        const float* x, const float* Wsrc, const int* found, double* part, int nblk, hipStream_t s,
-                       const SpecX* spec = nullptr, int qpair = 0);
+                       const SpecX* spec = nullptr, int qpair = 0, const SelectArgs* fsel = nullptr,
+                       const Hyper* fhp = nullptr, unsigned* fcount = nullptr);
+bool tail_select_fused(const Geom& g, int side);
 // after the x decision: zx = zc + X dWx for the gates whose exponent was mispredicted
 void launch_apply_fix(const Geom& g, const float* x, const float* dW, const float* zc, float* zx, const int* kpred,
                       const DevStats* stats, hipStream_t s);
@@ -259,7 +271,9 @@ void launch_x_l1max(const Geom& g, const float* x, float* range, hipStream_t s);
 bool qpair_ok(const Geom& g);
 bool qres_ok(const Geom& g);
 int q_layout(const Geom& g);   // 2 (bf16 row quads) or 0 (row-major f32)
-void launch_qgemm3(const Geom& g, const float* Sh, const float* G, float* gimg, float* Q, hipStream_t s);
+// gimg_ready: the image was already formed (launch_reduce_gh_img)
+void launch_qgemm3(const Geom& g, const float* Sh, const float* G, float* gimg, float* Q, hipStream_t s,
+                   bool gimg_ready = false);
 // decide the first passing k in this pass's window; on success update the weights
 struct SelectArgs {
   int side;                 // 0 x, 1 h
@@ -276,13 +290,20 @@ struct SelectArgs {
   int* pick;                // [4] exponent chosen in this pass, -1 if none
   DevStats* stats;
   const int* force;         // [8] forced exponents per (gate, side) (admm_debug_force; nullable)
+  // the persistent sweep's weight image (launch_sweep_wt's layout; nullable): every updated weight
+  // element's three split pieces are written there too, so the image of the new weights is ready for
+  // the sweep without a k_sweep_wt launch (every element of every gate weight is updated each step)
+  void* wt;
+  int wt_rows16;            // its layout: 16-row (H > 256) or 32-row tiles
+  int wt_xc;                // x chunks of the image (sweep_xc)
 };
 void launch_select(const Geom& g, const Hyper& hp, const SelectArgs& a, hipStream_t s);
 
 // ---- output weight wy (admm.py:246-280; admm.no_dual_y.py:226-249)
 int wy_splits(const Geom& g);
+// u_ready: U already holds this state's residual (k_ht_apply of the previous step wrote it)
 void launch_wy_grad(const Geom& g, const Hyper& hp, const float* Sh, const float* a, const float* Ly,
-                    const float* wy, float* U, float* slab, int nsplit, hipStream_t s);
+                    const float* wy, float* U, float* slab, int nsplit, hipStream_t s, bool u_ready = false);
 // wy_apply non-null: also wy <- update(wy, G_y) in the same launch (no all-reduce of G_y needed)
 void launch_wy_reduce(const Geom& g, const Hyper& hp, const float* slab, int nsplit, float* Gy, float* wy_apply,
                       hipStream_t s);
@@ -293,8 +314,10 @@ int ht_blocks(const Geom& g);
 void launch_ht_partial(const Geom& g, const Hyper& hp, const Planes6& S, const Planes6& L, const float* a,
                        const float* Ly, const float* wy, double* part, int nblk, hipStream_t s);
 void launch_ht_reduce(const double* part, int nblk, double* sums, hipStream_t s);
+// U: also the next wy stage's residual; xbuf (nullable): also zero the column-split sweep's hand-off
+// buffer (sweep_xbuf_bytes) for the next step's sweep
 void launch_ht_apply(const Geom& g, const Hyper& hp, const Planes6& S, const Planes6& L, float* a, float* Ly,
                      const float* y, const float* wy, const double* sums, DevStats* stats, int* status, hipStream_t s,
-                     const int* force = nullptr);
+                     const int* force = nullptr, float* U = nullptr, void* xbuf = nullptr);
 
 }  // namespace admm

@@ -526,8 +526,9 @@ bool qres_ok(const Geom& g) { return g.H == 256 && qpair_ok(g) && g.BT() * 256 *
 
 int q_layout(const Geom& g) { return qpair_ok(g) ? 2 : 0; }
 
-void launch_qgemm3(const Geom& g, const float* Sh, const float* G, float* gimg, float* Q, hipStream_t s) {
-  launch_split_g(g, G, gimg, s);
+void launch_qgemm3(const Geom& g, const float* Sh, const float* G, float* gimg, float* Q, hipStream_t s,
+                   bool gimg_ready) {
+  if (!gimg_ready) launch_split_g(g, G, gimg, s);
   const bf16x8* gb = reinterpret_cast<const bf16x8*>(gimg);
   if (qres_ok(g)) {   // G resident in LDS: one workgroup per CU
     k_qgemm_res<<<256, 64 * QR_WAVES, 0, s>>>(g, Sh, gb, Q, nullptr);

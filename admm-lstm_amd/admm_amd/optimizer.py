@@ -274,10 +274,12 @@ class AdmmOptimizerBase(object):
         """In-place versions of every tensor the library's caches are derived from: the z
         cache (x, the eight gate weights, h) and the x stage's targets tgt = dual/rho + gate
         (the i, f, g, o gate and dual planes), plus c and the remaining duals, which the
-        library treats as known (dual h is zero before T unless the caller writes it)."""
+        library treats as known (dual h is zero before T unless the caller writes it), and the
+        next wy stage's residual rho_y (h_T wy - a - dual_y / rho_y) (model.out, a, dual y)."""
         m = self.model
-        ts = ([self._x] + [getattr(m, f'{s}2{q}') for s in 'xh' for q in GATES4]
-              + [self.gates[q] for q in GATES6] + [self.duals[q] for q in GATES6])
+        ts = ([self._x] + [getattr(m, f'{s}2{q}') for s in 'xh' for q in GATES4] + [m.out]
+              + [self.gates[q] for q in GATES6] + [self.duals[q] for q in GATES6]
+              + [self.gates['a'], self.duals['y']])
         return tuple(t._version for t in ts)
 
     def _snapshot(self) -> None:

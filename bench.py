@@ -325,6 +325,13 @@ def cpu_baseline(cfg_name: str, timed_steps: int = 5, crosscheck_threads: int = 
     model, sockets, per_socket = host_cpu()
     cores, socket, how = gpu_socket_cores(0)
     quota = cgroup_cpus()
+    # The protocol's "all physical cores of the GPU-local socket" is bounded by the CPU time this
+    # process may use: under a cgroup quota of Q CPUs, more than Q threads only time-share them (on the
+    # GPU box, 64 threads under a 16-CPU quota ran 64.9 s/it against 20 s on 16: profiles/
+    # r05c_c3_bench_cpu64_throttled.json), so the threads are the socket's cores up to the quota
+    if quota and quota >= 1 and int(quota) < len(cores):
+        how += f'; {int(quota)} of its {len(cores)} cores (cgroup CPU quota {quota})'
+        cores = cores[:int(quota)]
     old_aff = os.sched_getaffinity(0) if hasattr(os, 'sched_getaffinity') else None
     old_threads = torch.get_num_threads()
     threads = len(cores)

@@ -178,6 +178,7 @@ int main(int argc, char** argv) {
     float* rg; (void)hipMalloc(&rg, 64); (void)hipMemset(rg, 0, 64);
     if (!getenv("KB_NORANGE")) sw.range = rg;
     if (getenv("KB_NOTGT")) { sw.tgt = nullptr; sw.gx_slab = nullptr; }
+    if (getenv("KB_NOGXF")) sw.gx_slab = nullptr;   // tgt planes without the G_x fold
   }
   timeit("sweep_t (t=5)", f4 * g.B * (g.D + 27.0 * g.H), 2.0 * g.B * (g.D + g.H) * 4 * g.H,
          [&] { launch_sweep_t(g, 5, w, hp, sw, s); });

@@ -64,7 +64,8 @@ class AdmmStats(Structure):
     _fields_ = [('steps', c_int32), ('k', c_int32 * 8), ('passes', c_int32 * 2), ('f_w', c_double * 8),
                 ('grad_sq', c_double * 8), ('theta_h', c_float), ('unresolved', c_int32), ('nonfinite', c_int32),
                 ('direct_frac', c_double * 8), ('handoff_fail', c_int32), ('sweep_fallbacks', c_int32),
-                ('graph_captures', c_int32), ('graph_disabled', c_int32), ('graph_replays', c_int64)]
+                ('graph_captures', c_int32), ('graph_disabled', c_int32), ('graph_replays', c_int64),
+                ('sweep_split_off', c_int32)]
 
 
 # name -> (restype, argtypes)

@@ -86,6 +86,8 @@ struct StepSig {   // admm_step's launch-sequence signature (see step_sig)
 };
 constexpr int kMaxOutputs = 4096;
 
+constexpr int kSweepFallbackLimit = 3;   // AdmmCtx::cs_off
+
 struct AdmmCtx {
   Geom g{};
   Hyper hp{};
@@ -141,6 +143,10 @@ struct AdmmCtx {
   // column-split sweep (strong-scaling ranks, sweep_rows_nc > 1): the h_t hand-off granules
   float* xbuf = nullptr;
   bool cs_poison = false;   // test hook (ADMM_SWEEP_SPLIT_COLS=2)
+  // the column split is turned off for the context once kSweepFallbackLimit of its launches found
+  // their grid not resident (each such step paid the entry wait, up to 2 ms, before the row-block
+  // sweep ran): from then on the row-block sweep runs directly
+  bool cs_off = false;
   // pass 0 of a gate whose last exponent was past the first window also sums the per-candidate
   // elements' polynomial, so the exponents past it are decided without pass 1 (ADMM_P16=0: off)
   bool p16 = true;
@@ -477,7 +483,9 @@ int stage_sweep(AdmmCtx* c, hipStream_t s) {
     }
     sa.lamh_nz = c->lamh_known && c->lamh_skip ? c->lamh_nz : nullptr;
     sa.range = c->range;   // zeroed by this step's h-stage k_reduce_g
-    sa.xbuf = c->xbuf;     // zeroed by k_sweep_wt (column split only)
+    if (c->xbuf && !c->cs_off && ((const volatile int*)c->status_host)[3] >= kSweepFallbackLimit)
+      c->cs_off = true;    // (the mirror: fallbacks as of the last completed step)
+    sa.xbuf = c->cs_off ? nullptr : c->xbuf;   // zeroed by k_sweep_wt (column split only)
     sa.fail = &c->stats->handoff_fail;       // a hand-off that timed out makes the step's results invalid
     sa.fallback = &c->stats->sweep_fallback;  // the column split's grid was not resident: row-block sweep ran
     sa.skip_publish = c->fault_skip_publish ? 1 : 0;
@@ -488,7 +496,7 @@ int stage_sweep(AdmmCtx* c, hipStream_t s) {
       launch_sweep_wt(g, w, c->swt, s, c->xbuf);
       c->wt_init = true;
     }
-    if (c->cs_poison && c->xbuf) sweep_poison_entry(g, c->xbuf, s);
+    if (c->cs_poison && sa.xbuf) sweep_poison_entry(g, c->xbuf, s);
     launch_sweep_rows(g, c->swt, c->hp, sa, s);
   } else {
     // Samples are independent across the sweep: two halves on two streams run their
@@ -796,7 +804,7 @@ StepSig step_sig(const AdmmCtx* c) {
   g.flags = (c->z_valid ? 1u : 0u) | (c->tgt_valid ? 2u : 0u) | (c->gx_valid ? 4u : 0u) | (c->range_valid ? 8u : 0u) |
             (c->x1_valid ? 16u : 0u) | (c->lamh_known ? 32u : 0u) | (c->hp.with_dual_y ? 64u : 0u) |
             (c->force_on ? 128u : 0u) | (c->prof_mask ? 256u : 0u) | (c->host_ar ? 512u : 0u) | (c->u_valid ? 1024u : 0u) |
-            (c->wt_init ? 2048u : 0u);
+            (c->wt_init ? 2048u : 0u) | (c->cs_off ? 4096u : 0u);
   g.buf = c->buf;
   g.trace[0] = c->trace_g[0]; g.trace[1] = c->trace_g[1]; g.trace[2] = c->trace_r[0]; g.trace[3] = c->trace_r[1];
   g.comm = c->comm;
@@ -1018,6 +1026,7 @@ int admm_get_stats(AdmmCtx* c, AdmmStats* out) {
   out->graph_captures = c->graph_captures;
   out->graph_disabled = c->graph_disabled ? 1 : 0;
   out->graph_replays = c->graph_replays;
+  out->sweep_split_off = c->cs_off ? 1 : 0;
   return ADMM_OK;
 }
 

@@ -320,7 +320,8 @@ class AdmmOptimizerBase(object):
             warning(f'{nonfin.value - seen[1]} non-finite line-search objective value(s) seen.')
         if fb.value > seen[2]:
             warning(f'{fb.value - seen[2]} column-split sweep launch(es) could not have their whole grid resident '
-                    f'(another kernel or process on the GPU?): the row-block sweep ran instead (slower, same result).')
+                    f'(another kernel or process on the GPU?): the row-block sweep ran instead (slower, same result); '
+                    f'from the third one on this optimizer runs the row-block sweep directly.')
         self._status_seen = (unres.value, nonfin.value, fb.value)
 
     # ------------------------------------------------------------------ extras
@@ -343,6 +344,7 @@ class AdmmOptimizerBase(object):
             'graph_captures': s.graph_captures,
             'graph_disabled': bool(s.graph_disabled),
             'graph_replays': s.graph_replays,
+            'sweep_split_off': bool(s.sweep_split_off),
         }
 
     # ------------------------------------------------------------------ checkpoint

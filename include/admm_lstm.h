@@ -104,6 +104,8 @@ typedef struct AdmmStats {
   int32_t graph_captures;     /* ADMM_GRAPH=1: step graphs captured */
   int32_t graph_disabled;     /* 1 once a capture failed: steps run eagerly from then on */
   int64_t graph_replays;      /* steps run as a replay of a captured graph */
+  int32_t sweep_split_off;    /* 1 once 3 column-split launches fell back: the context then runs the
+                                 row-block sweep directly (no entry wait per step) */
 } AdmmStats;
 
 typedef struct AdmmCtx AdmmCtx;

@@ -34,6 +34,17 @@ class Golden:
     def compact(self):
         return self.meta.get('compact')
 
+    @property
+    def source(self):
+        """'reference' (made by importing /root/reference: tests/golden/make_golden.py) or 'oracle'
+        (made by this repo's CPU restatement where the reference cannot run: tools/make_c5g.py, C5's
+        global batch needs > 64 GB in the reference).  An oracle fixture pins the library to the oracle
+        (oracle consistency), not to the reference."""
+        src = self.meta.get('source')
+        if src is None:   # fixtures written before the key existed: the generator says which
+            src = 'oracle' if 'oracle/admm_oracle.py' in self.meta.get('generator', '') else 'reference'
+        return src
+
     def _inputs(self):
         if 'xy' not in self.__dict__:
             if self.compact:
@@ -117,5 +128,8 @@ _NAMES = sorted(f[:-4] for f in os.listdir(GOLDEN) if f.endswith('.npz') and not
 # tests/test_gpu_weight_phase.py runs them
 PERTURBED = [n for n in _NAMES if Golden(n).meta.get('perturb')]
 COMPACT = [n for n in _NAMES if Golden(n).compact and n not in PERTURBED]
+# full-size fixtures the reference itself produced, and those the oracle produced (c5g)
+COMPACT_REF = [n for n in COMPACT if Golden(n).source == 'reference']
+COMPACT_ORACLE = [n for n in COMPACT if Golden(n).source == 'oracle']
 ALL = [n for n in _NAMES if n not in COMPACT and n not in PERTURBED]
 FULL = [n for n in ALL if Golden(n).full_state]

@@ -28,7 +28,7 @@ import os
 import pytest
 import torch
 
-from golden_io import COMPACT, Golden
+from golden_io import COMPACT_ORACLE, COMPACT_REF, Golden
 from oracle import admm_oracle as O
 from test_gpu_parity import LOSS_RTOL, _loss, _optimizer
 
@@ -167,12 +167,32 @@ def _write(name, recs, g):
         json.dump({'steps': summ, 'orig_form': orig_form_departures(recs)}, f, indent=1)
 
 
-@pytest.mark.parametrize('name', COMPACT)
+@pytest.mark.parametrize('name', COMPACT_REF)
 def test_fullsize_matches_reference(name, dev):
     g = Golden(name)
+    assert g.source == 'reference'
     mods = _load_mods()
-    recs = _run(g, mods, dev, arbitrate={'c3': 'all', 'c5g': 'none'}.get(name, 'lazy'))
+    recs = _run(g, mods, dev, arbitrate='all' if name == 'c3' else 'lazy')
     _write(name, recs, g)
+    _check_fullsize(recs, g.T)
+
+
+@pytest.mark.parametrize('name', COMPACT_ORACLE)
+def test_fullsize_matches_oracle_fixture(name, dev):
+    """Oracle consistency, not reference parity: c5g (C5's global batch, B = 32 768) was made by the
+    CPU restatement run in fp32 on the GPU box (tools/make_c5g.py), because the reference needs more
+    than this container's 64 GB for it.  The oracle itself is pinned to the reference by the other
+    fixtures (tests/test_oracle_golden.py); here the same loss / weight bars apply, and every exponent
+    is arbitrated by the same-input fp64 search instead of the fixture's fp32 decisions."""
+    g = Golden(name)
+    assert g.source == 'oracle'
+    mods = _load_mods()
+    recs = _run(g, mods, dev, arbitrate='none')
+    _write(name, recs, g)
+    _check_fullsize(recs, g.T)
+
+
+def _check_fullsize(recs, T):
     for r in recs:
         s = r['step']
         assert r['loss'] == pytest.approx(r['ref_loss'], rel=LOSS_RTOL), (s, r['loss'], r['ref_loss'])
@@ -191,7 +211,7 @@ def test_fullsize_matches_reference(name, dev):
             assert a == k64 or (margin < tie and abs(a - k64) <= 1), (s, i, r['k'], r['ref_k'], r['fp64'],
                                                                         r['g_rel_diff'])
     _check_follows_fp64(recs)
-    check_orig_form(recs, g.T)
+    check_orig_form(recs, T)
 
 
 def _check_follows_fp64(recs):

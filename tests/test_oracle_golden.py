@@ -8,7 +8,8 @@ operands, and the full primal/dual state.
 import pytest
 import torch
 
-from golden_io import ALL, FULL, GATES6, PERTURBED, WEIGHT_NAMES, Golden, perturb_state
+from golden_io import (ALL, COMPACT_ORACLE, COMPACT_REF, FULL, GATES6, PERTURBED, WEIGHT_NAMES, Golden,
+                       perturb_state)
 from oracle import admm_oracle as O
 
 FAST = [n for n in ALL if not n.startswith('t1_')] + ['t1_gstock']
@@ -109,3 +110,15 @@ def test_dead_searches_are_dead():
         for rec in g.searches:
             assert rec['wy_true'] == 0 and rec['c_true'] == 0
             assert rec['c_count'] == g.T
+
+
+def test_fixture_sources():
+    """Every fixture says who made it: the reference (tests/golden/make_golden.py) for all
+    but c5g, which the oracle made (tools/make_c5g.py) and which is therefore only an oracle-consistency
+    case (test_gpu_fullsize.test_fullsize_matches_oracle_fixture)."""
+    assert COMPACT_ORACLE == ['c5g']
+    assert set(COMPACT_REF) == {'c3', 'c5_1gpu', 'c4g'}
+    for n in ALL + PERTURBED + COMPACT_REF:
+        g = Golden(n)
+        assert g.source == 'reference', n
+        assert g.meta.get('generator', 'tests/golden/make_golden.py').startswith('tests/golden/make_golden.py'), n

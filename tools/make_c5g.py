@@ -68,6 +68,7 @@ def main(out):
         'steps': STEPS, 'full_state': False, 'param_set': 'GoogleStock', 'params': pdict, 'losses': losses,
         'val_losses': [None] * (STEPS + 1), 'searches': searches, 'torch': torch.__version__,
         'threads': torch.get_num_threads(), 'step_times': times,
+        'source': 'oracle',   # an oracle fixture (tests/golden_io.py Golden.source), not a reference one
         'generator': 'tools/make_c5g.py: oracle/admm_oracle.py (the reference op structure) in fp32 on the GPU box '
                      '(the reference itself needs > 64 GB for this batch)',
         'device': torch.cuda.get_device_name(0),

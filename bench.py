@@ -592,6 +592,10 @@ def main():
             'line_search_k': list(stats['k'].values()),
             'trial_passes': stats['passes'],
             'direct_frac': [round(v, 4) for v in stats['direct_frac'].values()],
+            # column-split sweep health on rank 0: fallbacks to the row-block sweep and
+            # whether the context has turned the split off; hand-off timeouts would have raised
+            'sweep': {'fallbacks': stats['sweep_fallbacks'], 'split_off': stats['sweep_split_off'],
+                      'handoff_fail': stats['handoff_fail']},
             'final_train_mse': loss,
         }
         print(json.dumps(out), flush=True)

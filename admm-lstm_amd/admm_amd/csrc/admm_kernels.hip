@@ -1673,6 +1673,10 @@ __device__ __forceinline__ void dq_hint(DirectQ& dq, int pass, const int* found,
 
 // sw = f2 sg w (the pushed entry): w = |z| (sigmoid) or 2|z| (tanh) with the sign of z; E and
 // r = sigma(w) are re-formed here exactly as trial_point / trial_pair formed them
+#ifndef DC_ABL
+#define DC_ABL 0   // timing ablations for tools/kbench (wrong sums): 1 no candidate loop, 2 four candidates,
+                   // 4 no queue (profiles/r05k_trial_gate_imbalance.txt)
+#endif
 template <bool TANH>
 __device__ __forceinline__ void direct_candidates(float sw, float e, float d2, float (&acc)[kSlots], const DirectQ& dq) {
   const float w = fabsf(sw);
@@ -1715,9 +1719,11 @@ __device__ __forceinline__ void direct_candidates(float sw, float e, float d2, f
   // remainder past it, so its share 2 d0 D_lin / s goes into the s^1 polynomial coefficient
   // (used from pass 0 only; the scale is pass 0's smallest candidate 2^-(J-1))
   acc[kSlotPoly + 0] -= d2 * ((cr * (-E * e)) * r) * (float)(1 << (kTrialJ - 1));
+  if (DC_ABL & 1) return;
+  constexpr int kLo = (DC_ABL & 2) ? kTrialJ - 4 : 0;
   if (fabsf(e) * (float)(1 << (kTrialJ - 1)) <= 20.f) {   // |e| <= 20 on every candidate: no exp
 #pragma unroll
-    for (int k = kTrialJ - 1; k >= 0; --k) {
+    for (int k = kTrialJ - 1; k >= kLo; --k) {
       const float y = E * m;
       const float D = (cr * y) * __builtin_amdgcn_rcpf(one_e + y);
       acc[k] = fmaf(D, d2 + D, acc[k]);
@@ -1726,7 +1732,7 @@ __device__ __forceinline__ void direct_candidates(float sw, float e, float d2, f
     return;
   }
 #pragma unroll
-  for (int k = kTrialJ - 1; k >= 0; --k) {
+  for (int k = kTrialJ - 1; k >= kLo; --k) {
     const float yb = fminf(__expf(-e - w), kCap);
     const float y = -e > 20.f ? yb : E * m;
     const float D = (cr * y) * __builtin_amdgcn_rcpf(one_e + y);
@@ -1739,6 +1745,7 @@ __device__ __forceinline__ void direct_candidates(float sw, float e, float d2, f
 // An entry is (sw, e, d2): sw = the signed w (E, r and the sign are re-formed from it when the
 // entry runs, one v_exp and one v_rcp per 64 entries instead of two more LDS words per push).
 __device__ __forceinline__ void dq_push(DirectQ& dq, bool p, float sw, float e, float d2) {
+  if (DC_ABL & 4) p = false;
   const unsigned long long m = __builtin_amdgcn_ballot_w64(p);
   if (p) {
     // this lane's rank among the pushing lanes: v_mbcnt_lo / v_mbcnt_hi on the ballot

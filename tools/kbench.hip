@@ -134,6 +134,34 @@ int main(int argc, char** argv) {
     }
     return 0;
   }
+  if (mode == "trg") {   // gate imbalance: only gate 2 (g, tanh) in the per-candidate regime, as in the step
+    const size_t ng = (size_t)g.D * g.H;
+    std::vector<float> gh(4 * ng);
+    (void)hipMemcpy(gh.data(), G, gh.size() * 4, hipMemcpyDeviceToHost);
+    float* Gbig; (void)hipMalloc(&Gbig, gh.size() * 4);
+    float* Gmix; (void)hipMalloc(&Gmix, gh.size() * 4);
+    std::vector<float> gb(gh), gm(gh);
+    for (auto& v : gb) v *= 100.f;                                    // |q| = |x G| ~ 0.5: per-candidate
+    for (size_t i = 2 * ng; i < 3 * ng; ++i) gm[i] *= 100.f;          // gate 2 only
+    (void)hipMemcpy(Gbig, gb.data(), gb.size() * 4, hipMemcpyHostToDevice);
+    (void)hipMemcpy(Gmix, gm.data(), gm.size() * 4, hipMemcpyHostToDevice);
+    float* Qb = dev_random(4 * n, -1.f, 1.f, 7);
+    float* Qmix = dev_random(4 * n, -1e-4f, 1e-4f, 4);
+    (void)hipMemcpy(Qmix + 2 * n, Qb + 2 * n, n * 4, hipMemcpyDeviceToDevice);
+    // the step's grids (KB_NB0 / KB_NB1: overrides for a scan)
+    const int nb0 = getenv("KB_NB0") ? atoi(getenv("KB_NB0")) : trial_fast_blocks(g, 0);
+    const int nb1 = getenv("KB_NB1") ? atoi(getenv("KB_NB1")) : trial_fast_blocks(g, 1);
+    printf("trial grids: x %d, h %d workgroups per gate and column block\n", nb0, nb1);
+    for (int r = 0; r < 3; ++r) {
+      timeit("x trials, all poly", f4 * 2 * 4 * n, 0, [&] { launch_trial_fast(g, 0, 0, zc, tgt, nullptr, x, G, found, part, nb0, s); });
+      timeit("x trials, g direct", f4 * 2 * 4 * n, 0, [&] { launch_trial_fast(g, 0, 0, zc, tgt, nullptr, x, Gmix, found, part, nb0, s); });
+      timeit("x trials, all direct", f4 * 2 * 4 * n, 0, [&] { launch_trial_fast(g, 0, 0, zc, tgt, nullptr, x, Gbig, found, part, nb0, s); });
+      timeit("h trials, all poly", f4 * 3 * 4 * n, 0, [&] { launch_trial_fast(g, 1, 0, zc, tgt, Q, x, dW, found, part, nb1, s, nullptr, 0); });
+      timeit("h trials, g direct", f4 * 3 * 4 * n, 0, [&] { launch_trial_fast(g, 1, 0, zc, tgt, Qmix, x, dW, found, part, nb1, s, nullptr, 0); });
+      timeit("h trials, all direct", f4 * 3 * 4 * n, 0, [&] { launch_trial_fast(g, 1, 0, zc, tgt, Qb, x, dW, found, part, nb1, s, nullptr, 0); });
+    }
+    return 0;
+  }
   if (mode == "tr") {   // the two pass-0 trial kernels alone
     for (int r = 0; r < 3; ++r) {
       timeit("trial_fast side0", f4 * 2 * 4 * n, 0, [&] { launch_trial_fast(g, 0, 0, zc, tgt, nullptr, x, G, found, part, nb, s); });

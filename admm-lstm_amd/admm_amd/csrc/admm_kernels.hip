@@ -3818,13 +3818,17 @@ bool trial_rows_ok(const Geom& g) { return g.H % 256 == 0; }
 // workgroups per gate (and column block) of the fast trial passes.  Each walks the rows with a
 // stride of that many tiles, so few rows per GPU leave each workgroup few tiles to amortise its
 // setup and its epilogue (the 38-slot block reduction) over: at B = 1024 the x trials (k_trial_mx)
-// take 111 / 99 / 92 us with 512 / 256 / 128 workgroups (tools/kbench "tr", KB_NB), so they get at
-// least 16 tiles per workgroup; at B = 8192 (512: 513 us, 256: 509) and for the h trials the
-// streaming count stays.  Never more than stream_blocks(g): the partial buffer is sized for it.
+// take 111 / 99 / 92 us with 512 / 256 / 128 workgroups when every gate is in the polynomial regime
+// (tools/kbench "tr", KB_NB).  But the step's g gate is mostly in the per-candidate regime, which
+// costs its workgroups 2-3x the others', and with a single round of workgroups the CUs of the other
+// gates then idle: with that mix (kbench "trg") 128 / 256 / 512 workgroups take 151 / 109 / 113 us
+// (profiles/r05n_trial_grid_scan.txt).  So at least 8 tiles per workgroup (256 at B = 1024); at
+// B = 8192 and for the h trials the streaming count stays.  Never more than stream_blocks(g): the
+// partial buffer is sized for it.
 int trial_fast_blocks(const Geom& g, int side) {
   const int sb = stream_blocks(g);
   if (side == 0 && trial_mx_ok(g)) {
-    const int64_t nb = (g.BT() + 15) / 16 / 16;   // >= 16 tiles per workgroup
+    const int64_t nb = (g.BT() + 15) / 16 / 8;   // >= 8 tiles per workgroup
     return (int)std::min<int64_t>(sb, std::max<int64_t>(64, nb));
   }
   return sb;

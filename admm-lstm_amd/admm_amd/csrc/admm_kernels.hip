@@ -1722,12 +1722,19 @@ __device__ __forceinline__ void direct_candidates(float sw, float e, float d2, f
   if (DC_ABL & 1) return;
   constexpr int kLo = (DC_ABL & 2) ? kTrialJ - 4 : 0;
   if (fabsf(e) * (float)(1 << (kTrialJ - 1)) <= 20.f) {   // |e| <= 20 on every candidate: no exp
+    // two candidates at a time on packed f32 operations (v_pk_mul / v_pk_add), the same operations
+    // per candidate as the scalar loop below, so the same bits
+    typedef float f2 __attribute__((ext_vector_type(2)));
 #pragma unroll
-    for (int k = kTrialJ - 1; k >= kLo; --k) {
-      const float y = E * m;
-      const float D = (cr * y) * __builtin_amdgcn_rcpf(one_e + y);
-      acc[k] = fmaf(D, d2 + D, acc[k]);
-      m = m * (m + 2.f);
+    for (int k = kTrialJ - 1; k >= kLo + 1; k -= 2) {
+      const float m1 = m * (m + 2.f);   // candidate k - 1
+      const f2 y = E * f2{m, m1};
+      const f2 den = one_e + y;
+      const f2 D = (cr * y) * f2{__builtin_amdgcn_rcpf(den.x), __builtin_amdgcn_rcpf(den.y)};
+      const f2 dd = d2 + D;
+      acc[k] = fmaf(D.x, dd.x, acc[k]);
+      acc[k - 1] = fmaf(D.y, dd.y, acc[k - 1]);
+      m = m1 * (m1 + 2.f);
     }
     return;
   }

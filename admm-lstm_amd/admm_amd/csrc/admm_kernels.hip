@@ -1627,10 +1627,11 @@ __global__ __launch_bounds__(kThreads) void k_qgemm(Geom g, const float* x, cons
 // Trial pass.  For the line search (admm.py:316-336) each gate needs, for k = 0, 1, ...,
 //   f(W + G/2^k) - f(W) = 0.5 rho sum_e [ (d0 + D_k)^2 - d0^2 ],  D_k = phi(z + q 2^-k) - phi(z),
 // evaluated without cancellation (DESIGN.md "line-search numerics").  Two regimes per element:
-//  * |q| <= 2^-5 (the common case): D_k = sum_{n<=5} a_n s^n with s = 2^-k and a_n = c_n q^n
-//    (5-term Taylor: truncation |c6/c1| (qs)^5 <= 2e-8 relative to D for every k >= 0), so the
-//    increment is a degree-10 polynomial in s whose 10 coefficients are summed once (pass 0)
-//    and cover every exponent;
+//  * |q| <= kPolyQ = 2^-4 (the common case): D_k = sum_{n<=5} a_n s^n with s = 2^-k and a_n = c_n q^n
+//    (5-term Taylor: truncation |c6/c1| (qs)^5, about 1e-7 of D for tanh at qs = 2^-4 and 2^-5 times
+//    less per exponent beyond; round 3's bound 2^-5 gave 3e-9 but left most of the g gate's elements
+//    to the per-candidate loop), so the increment is a degree-10 polynomial in s whose
+//    10 coefficients are summed once (pass 0) and cover every exponent;
 //  * otherwise: D_k per candidate of the pass window k in [pass*J, pass*J + J), branch-free
 //    (see trial_direct).
 // Slot layout per gate: kSlots = [J candidates][6 poly][sum d0^2][#per-candidate elements].
@@ -1686,7 +1687,7 @@ __device__ __forceinline__ void direct_candidates(float sw, float e, float d2, f
   const float cr = -F * r;
   if (dq.hi) {
     // the element's Taylor polynomial in s for k >= kTrialJ: D = sum_n a_n s^n, a_n = F c_n(w) E0^n,
-    // E0 = e 2^(J-1) = F q (pass 0), valid while |E0| s <= 2^-5; remainder coefficients of s^2..s^10
+    // E0 = e 2^(J-1) = F q (pass 0), valid while |E0| s <= kPolyQ; remainder coefficients of s^2..s^10
     const int lane = threadIdx.x & 63;
     const float E0 = e * (float)(1 << (kTrialJ - 1));
     if (fabsf(E0) <= kPolyQ * (float)(1 << kTrialJ)) {

@@ -9,7 +9,11 @@ namespace admm {
 constexpr int kTrialJ = 16;      // line-search candidates evaluated per trial pass
 // per-gate sums of a trial pass: [J candidates][10 polynomial coefficients][sum d0^2][#per-candidate elements]
 constexpr int kPolyN = 10;
-constexpr float kPolyQ = 0x1p-5f;   // |q| bound of the polynomial (5-term Taylor) regime
+// |q| bound of the polynomial (5-term Taylor) regime, 2^-KPOLYQ_LOG2 (admm_kernels.hip "Trial pass")
+#ifndef KPOLYQ_LOG2
+#define KPOLYQ_LOG2 4
+#endif
+constexpr float kPolyQ = 1.0f / (float)(1 << KPOLYQ_LOG2);
 // + pass 0's second polynomial (kPolyHiN coefficients of s^2..s^10 over the per-candidate
 // elements, valid for k >= kTrialJ) and the count of elements it cannot cover
 constexpr int kPolyHiN = 9;

@@ -266,9 +266,9 @@ def test_trial_increments_vs_fp64(tanh_gate, pair, dev):
 @pytest.mark.parametrize('pair', [0, 2])
 @pytest.mark.parametrize('tanh_gate', [0, 1])
 def test_trial_polynomial_band_vs_fp64(tanh_gate, pair, dev):
-    """Elements at the top of the polynomial regime (|q| in [2^-9, 2^-5]: 5-term Taylor in s,
-    admm_kernels.hpp kPolyQ), every exponent of the first two windows, vs numpy fp64 (the
-    remainder past the first-order term, as test_trial_increments_vs_fp64)."""
+    """Elements at the top of the polynomial regime (|q| in [2^-9, 2^-4]: 5-term Taylor in s,
+    admm_kernels.hpp kPolyQ = 2^-KPOLYQ_LOG2), every exponent of the first two windows, vs numpy fp64
+    (the remainder past the first-order term, as test_trial_increments_vs_fp64)."""
     from admm_amd import _native as N
     lib = N.load()
     rng = np.random.default_rng(6)
@@ -276,7 +276,7 @@ def test_trial_polynomial_band_vs_fp64(tanh_gate, pair, dev):
     z = rng.normal(0, 2.5, n).astype(np.float32)
     phi = np.tanh if tanh_gate else (lambda v: 1 / (1 + np.exp(-v)))
     tgt = (phi(z.astype(np.float64)) + rng.normal(0, 1e-3, n)).astype(np.float32)
-    q = (rng.choice([-1.0, 1.0], n) * 2.0 ** rng.uniform(-9, -5, n)).astype(np.float32)
+    q = (rng.choice([-1.0, 1.0], n) * 2.0 ** rng.uniform(-9, -4, n)).astype(np.float32)
     zt, tt, qt = (torch.from_numpy(a).to(dev) for a in (z, tgt, q))
     # reference in x87 extended precision: the remainder D^2 + 2 d0 (D - s phi' q) cancels D's
     # first-order part, which fp64 D (absolute error ~1e-16) no longer resolves at s <= 2^-16

@@ -2413,33 +2413,37 @@ __device__ __forceinline__ void trial_rows_body(const Geom& g, int q, int pass, 
 #ifndef TR_MINB
 #define TR_MINB 1   // workgroups per CU the register allocation must allow
 #endif
-// The three split pieces of the updated weight element i (row i / H of x2q or h2q, column i % H) at
-// their places in the persistent sweep's weight image (k_sweep_wt / k_sweep_wt16 layouts).
-__device__ __forceinline__ void sweep_wt_put(const SelectArgs& a, const Geom& g, int q, int64_t i, float w) {
+// The three split pieces of updated weight elements k0 .. k0 + 7 (rows of x2q or h2q, k0 % 8 == 0) of
+// column jj, as the three bf16x8 the sweep image holds them in (one 16-byte store per piece; rows past
+// Kd are the image's zero padding and are given zeros)
+__device__ __forceinline__ void sweep_wt_put8(const SelectArgs& a, const Geom& g, int q, int k0, int jj,
+                                              const float (&w)[8]) {
   const int H = g.H;
-  const int k = (int)(i / H), jj = (int)(i - (int64_t)k * H);
-  __bf16 p[3];
-  split3(w, p[0], p[1], p[2]);
-  __bf16* wt = static_cast<__bf16*>(a.wt);
   int64_t base;
-  int e;
   if (a.wt_rows16) {   // k_sweep_wt16: chunk 32 deep, 64-column tiles of 4 column blocks
-    const int kk = (a.side == 0 ? 0 : 32 * a.wt_xc) + k;
+    const int kk = (a.side == 0 ? 0 : 32 * a.wt_xc) + k0;
     const int NT = H / 64, KC2 = a.wt_xc + H / 32;
     const int c = kk >> 5, kq = (kk & 31) >> 3, n = jj >> 6, jq = (jj & 63) >> 4;
     const int lane = (jj & 15) + 16 * kq;
     base = ((((int64_t)(q * NT + n) * KC2 + c) * 4 + jq) * 3) * 64 + lane;
-    e = kk & 7;
   } else {             // k_sweep_wt: chunk 16 deep, 32-column tiles
-    const int kk = (a.side == 0 ? 0 : 16 * a.wt_xc) + k;
+    const int kk = (a.side == 0 ? 0 : 16 * a.wt_xc) + k0;
     const int NT = H / 32, KC2 = a.wt_xc + 2 * NT;
     const int c = kk >> 4, h = (kk & 15) >> 3, n = jj >> 5;
     const int lane = (jj & 31) + 32 * h;
     base = (((int64_t)(q * NT + n) * KC2 + c) * 3) * 64 + lane;
-    e = kk & 7;
   }
+  bf16x8 p0, p1, p2;
 #pragma unroll
-  for (int pc = 0; pc < 3; ++pc) wt[(base + 64 * pc) * 8 + e] = p[pc];
+  for (int e = 0; e < 8; ++e) {
+    __bf16 b0, b1, b2;
+    split3(w[e], b0, b1, b2);
+    p0[e] = b0; p1[e] = b1; p2[e] = b2;
+  }
+  bf16x8* wt = static_cast<bf16x8*>(a.wt);
+  wt[base] = p0;
+  wt[base + 64] = p1;
+  wt[base + 128] = p2;
 }
 
 // k_select's work for gate q by block mb of nmb (the weight update is split over the nmb blocks).
@@ -2627,6 +2631,35 @@ __device__ __forceinline__ void select_gate(const Geom& g, const Hyper& hp, cons
   const WUpd u = WUpd::make(rho, beta, g.T, pick);
   float* W = a.W[q];
   const int64_t gstride = (int64_t)nmb * kThreads;
+  if (a.wt) {
+    // with the sweep image: 8-row groups of one column per thread (the W / G loads of a row stay
+    // coalesced across the block's threads; the image takes three 16-byte stores per group)
+    const int64_t ng = (int64_t)((Kd + 7) / 8) * g.H;
+    for (int64_t gi = (int64_t)mb * kThreads + tid; gi < ng; gi += gstride) {
+      const int kg = (int)(gi / g.H), jj = (int)(gi - (int64_t)kg * g.H);
+      float w0[8], gv[8], w1[8];
+#pragma unroll
+      for (int r = 0; r < 8; ++r) {
+        const int64_t i = (int64_t)(8 * kg + r) * g.H + jj;
+        const bool in = 8 * kg + r < Kd;
+        w0[r] = in ? W[i] : 0.f;
+        gv[r] = in ? Gq[i] : 0.f;
+      }
+#pragma unroll
+      for (int r = 0; r < 8; ++r) {
+        const int64_t i = (int64_t)(8 * kg + r) * g.H + jj;
+        if (8 * kg + r < Kd) {
+          w1[r] = u.apply(w0[r], gv[r]);
+          W[i] = w1[r];
+          if (a.dW) a.dW[(int64_t)q * nW + i] = w1[r] - w0[r];
+        } else {
+          w1[r] = 0.f;
+        }
+      }
+      sweep_wt_put8(a, g, q, 8 * kg, jj, w1);
+    }
+    return;
+  }
   int64_t i = (int64_t)mb * kThreads + tid;
   for (; !LIGHT && i + 3 * gstride < nW; i += 4 * gstride) {   // four elements' loads in flight
     float w0[4], gv[4];
@@ -2637,7 +2670,6 @@ __device__ __forceinline__ void select_gate(const Geom& g, const Hyper& hp, cons
       const float w1 = u.apply(w0[e], gv[e]);
       W[i + e * gstride] = w1;
       if (a.dW) a.dW[(int64_t)q * nW + i + e * gstride] = w1 - w0[e];
-      if (a.wt) sweep_wt_put(a, g, q, i + e * gstride, w1);
     }
   }
   for (; i < nW; i += gstride) {
@@ -2645,7 +2677,6 @@ __device__ __forceinline__ void select_gate(const Geom& g, const Hyper& hp, cons
     const float w1 = u.apply(w0, Gq[i]);
     W[i] = w1;
     if (a.dW) a.dW[(int64_t)q * nW + i] = w1 - w0;
-    if (a.wt) sweep_wt_put(a, g, q, i, w1);
   }
 }
 

@@ -129,6 +129,11 @@ int main(int argc, char** argv) {
       for (int q = 0; q < 4; ++q) sa.W[q] = W[side * 4 + q];
       sa.dW = side == 0 ? dW : nullptr;
       sa.found_in = fl; sa.found_out = fl + 4; sa.pick = pick; sa.stats = st;
+      if (!getenv("KB_NOWT")) {   // as in the step: the selection also writes the sweep's weight image
+        static float* wt = nullptr;
+        if (!wt) (void)hipMalloc(&wt, sweep_wt_floats(g) * 4);
+        sa.wt = wt; sa.wt_rows16 = sweep_wt_rows16(g); sa.wt_xc = sweep_wt_xc(g);
+      }
       char nm[64]; snprintf(nm, sizeof nm, "select side %d (nred %d)", side, nred);
       for (int r = 0; r < 3; ++r) timeit(nm, 0, 0, [&] { launch_select(g, hp, sa, s); });
     }

@@ -89,6 +89,8 @@ static void check_args() {
   CHECK(admm_get_stats(nullptr, &st) != ADMM_OK);
   int32_t u = 0, nf = 0;
   CHECK(admm_poll_status(nullptr, &u, &nf) != ADMM_OK);
+  CHECK(admm_poll_faults(nullptr, &u, &nf) == ADMM_EINVAL);     // ABI 2
+  CHECK(admm_debug_fault(nullptr, 1) == ADMM_EINVAL);
   CHECK(admm_profile(nullptr, 1) != ADMM_OK);
   CHECK(admm_set_comm(nullptr, nullptr, 0, 0, 1) == ADMM_EINVAL);
   CHECK(admm_set_comm_host(nullptr, nullptr, nullptr, 0, 1) != ADMM_OK);
@@ -235,6 +237,12 @@ static void run_context(int64_t B, int T, int D, int H, int O, int variant, int 
   CHECK(st.unresolved == 0 && st.nonfinite == 0);
   int32_t unres = -1, nonfin = -1;
   CHECK(admm_poll_status(ctx, &unres, &nonfin) == ADMM_OK);
+  int32_t hf = -1, fb = -1;   // ABI 2: fault counts (no column split fault in a healthy run)
+  CHECK(admm_poll_faults(ctx, &hf, &fb) == ADMM_OK && hf == 0);
+  CHECK(admm_poll_faults(ctx, nullptr, &fb) == ADMM_EINVAL);
+  CHECK(st.handoff_fail == 0 && st.graph_disabled == 0);
+  CHECK(admm_debug_fault(ctx, 0) == ADMM_OK);
+  CHECK(admm_debug_fault(ctx, 7) == ADMM_EINVAL);
   // z cache copy-out: too small a destination is refused, the right size is accepted
   const int64_t zbytes = (int64_t)4 * B * T * H * 4;
   float* zc = zeros((size_t)4 * B * T * H);

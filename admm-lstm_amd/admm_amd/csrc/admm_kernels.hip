@@ -582,10 +582,14 @@ __global__ __launch_bounds__(SR_THREADS) void k_sweep_rows(Geom g, const bf16x8*
     float xcur[8], xnext[NTC == 1 ? 1 : 8];
     int gxs = 0;
     auto load_gx_x = [&](int tn, float (&xv)[8]) {
+      // from an opaque copy of the lane index, so that the eight row addresses are formed per call:
+      // hoisted as loop invariants they were spilled (64-bit each) and reloaded one wait at a time
+      int ln = lane;
+      asm volatile("" : "+v"(ln));
 #pragma unroll
       for (int ks = 0; ks < 8; ++ks) {
-        const int64_t b = min(m0 + 4 * ks + (lane >> 4), a.r1 - 1);
-        const int d = lane & 15;
+        const int64_t b = min(m0 + 4 * ks + (ln >> 4), a.r1 - 1);
+        const int d = ln & 15;
         xv[ks] = d < D ? a.x[(b * T + (tn - 1)) * D + d] : 0.f;
       }
     };
@@ -913,13 +917,22 @@ __global__ __launch_bounds__(SR_THREADS) void k_sweep_rows(Geom g, const bf16x8*
     constexpr int OC = H - TW * NTC;               // other groups' columns
     constexpr int NP = ROWS * OC / 2 / 256;        // 16-byte granule pairs per consumer thread
     f32x4 gv[NP > 0 ? NP : 1];
+    // the granule addresses are formed here each t from an opaque copy of the thread index: hoisted
+    // out of the sweep's loop as loop invariants they took 2 NP registers for the whole kernel, which
+    // the GX variants spilled to scratch and reloaded one wait at a time every t
+    // (one constant division per exchange; granule pair i = ct + 256 i steps it by constants)
+    unsigned cto = (unsigned)ct;
+    if constexpr (NC < 8) asm volatile("" : "+v"(cto));
+    constexpr unsigned OC2 = OC > 0 ? OC / 2 : 1;   // (NC == 1 instantiates this with OC = 0, never called)
+    const unsigned q0 = cto / OC2, r0 = cto % OC2;
+    const uint32_t xo = (t & 1) * xset + (uint32_t)(rb * 32 * H * 8);
     auto addr = [&](int i, int& hr, int& col) {
-      const int f = ct + 256 * i;
-      constexpr int OC2 = OC > 0 ? OC / 2 : 1;   // (NC == 1 instantiates this with OC = 0, never called)
-      hr = f / OC2;
-      const int oc = 2 * (f % OC2);
+      unsigned r = r0 + (256u * i) % OC2, q = q0 + (256u * i) / OC2;
+      if (r >= OC2) { r -= OC2; ++q; }
+      hr = (int)q;
+      const int oc = 2 * (int)r;
       col = oc < TW * n0 ? oc : oc + TW * NTC;
-      return (t & 1) * xset + (uint32_t)(((rb * 32 + hr) * H + col) * 8);
+      return xo + (uint32_t)((hr * H + col) * 8);
     };
     const unsigned want = (unsigned)t;
     uint64_t t0 = 0;
@@ -997,7 +1010,12 @@ __global__ __launch_bounds__(SR_THREADS) void k_sweep_rows(Geom g, const bf16x8*
 #endif
       const St4 cur = nxt;
       if (NC > 1 && ct == 0) CS_STAMP(t, 0);
-      const float xm = GXC && rok ? a.x[bx * T + (t - 1)] : 0.f;   // GXC (D == 1): x_t of this row
+      float xm = 0.f;   // GXC (D == 1): x_t of this row (its address formed per tile: as a hoisted
+      if constexpr (GXC) {   // 64-bit invariant it was spilled)
+        int64_t bxo = bx;
+        asm volatile("" : "+v"(bxo));
+        xm = rok ? a.x[bxo * T + (t - 1)] : 0.f;
+      }
 #ifdef SR_TIMING
       asm volatile("" :: "v"(cur.f0), "v"(cur.g0), "v"(cur.c0), "v"(cur.h0), "v"(cur.li), "v"(cur.lf), "v"(cur.lg),
                    "v"(cur.lo), "v"(cur.lc), "v"(cur.lh), "v"(cur.cp));

@@ -33,6 +33,7 @@ CLASSES = [
     ('buffer/global loads', re.compile(r'^(buffer|global)_load')),
     ('buffer/global stores', re.compile(r'^(buffer|global)_store')),
     ('LDS (ds_)', re.compile(r'^ds_')),
+    ('scratch (VGPR spill loads/stores)', re.compile(r'^(scratch|buffer)_(load|store).*(scratch|off, s\[0:3\])|^scratch_')),
     ('MFMA', re.compile(r'^v_mfma')),
     ('SALU (s_ except waits/branches)', re.compile(r'^s_(?!waitcnt|cbranch|branch|barrier|nop)')),
     ('s_waitcnt', re.compile(r'^s_waitcnt')),

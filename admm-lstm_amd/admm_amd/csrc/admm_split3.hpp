@@ -93,7 +93,9 @@ __device__ __forceinline__ void qgemm3_tile(const Geom& g, const float* __restri
   // not cover the L2/HBM latency of the next operands); NK is even (H % 256 == 0)
   struct Slot { float4 a0, a1; bf16x8 b[BU / NT]; };
   auto gload = [&](Slot& r, int c) {
-    if (c >= NK) return;
+    // past the last step: step NK - 1 again, unused.  Skipping the loads instead (a branch) left the
+    // compiler's count of loads in flight unknown after it, and every step then waited for all of them
+    c = c < NK ? c : NK - 1;
     if (S3_ABL & 32) {
       r.a0 = make_float4(c, 1.f, 2.f, 3.f); r.a1 = r.a0;
     } else {
@@ -161,7 +163,10 @@ __device__ __forceinline__ void qgemm3_tile(const Geom& g, const float* __restri
     __builtin_amdgcn_sched_barrier(0);
     compute(1);
     __builtin_amdgcn_sched_barrier(0);
-    if (c + 2 < NK) lstore(0, R0);
+    // unconditional (the last one stores step NK - 1 again, never read): under `if (c + 2 < NK)`
+    // the compiler sank R0's loads into that branch, just before this store, and they lost their
+    // step of lead
+    lstore(0, R0);
     __syncthreads();
   }
 }

@@ -590,9 +590,10 @@ __global__ __launch_bounds__(SR_THREADS) void k_sweep_rows(Geom g, const bf16x8*
       for (int ks = 0; ks < 8; ++ks) {
         const int64_t b = min(m0 + 4 * ks + (ln >> 4), a.r1 - 1);
         const int d = ln & 15;
-        xv[ks] = d < D ? a.x[(b * T + (tn - 1)) * D + d] : 0.f;
+        xv[ks] = a.x[(b * T + (tn - 1)) * D + (d < D ? d : D - 1)];   // masked at use (gx_x)
       }
     };
+    const auto gx_x = [&](float v) { return (lane & 15) < D ? v : 0.f; };   // x operand lanes d < D
     auto gx_fold = [&](int buf) {
       if constexpr (NTC == 1) {
         load_gx_x(gxs + 1, xcur);   // off the critical path: the producer then waits at mid-step
@@ -607,7 +608,7 @@ __global__ __launch_bounds__(SR_THREADS) void k_sweep_rows(Geom g, const bf16x8*
       for (int ks = 0; ks < 8; ++ks)
 #pragma unroll
         for (int h = 0; h < 2; ++h)
-          gx[0][h] = __builtin_amdgcn_mfma_f32_16x16x4f32(xcur[ks], Rq[4 * ks * 32 + 16 * h], gx[0][h], 0, 0, 0);
+          gx[0][h] = __builtin_amdgcn_mfma_f32_16x16x4f32(gx_x(xcur[ks]), Rq[4 * ks * 32 + 16 * h], gx[0][h], 0, 0, 0);
       const f32x4 r0 = gx[0][0], r1 = gx[0][1];
 #pragma unroll
       for (int k = 0; k + 1 < NTC; ++k) {
@@ -747,11 +748,13 @@ __global__ __launch_bounds__(SR_THREADS) void k_sweep_rows(Geom g, const bf16x8*
     auto load_gx_x = [&](int tn, float (&xv)[8]) {   // A operand: x_tn[row 4ks + lane/16][d = lane%16]
 #pragma unroll
       for (int ks = 0; ks < 8; ++ks) {
+        // unmasked (d clamped): a select here would wait for the load; gx_x masks it at its use
         const int64_t b = min(m0 + 4 * ks + (lane >> 4), a.r1 - 1);
         const int d = lane & 15;
-        xv[ks] = d < D ? a.x[(b * T + (tn - 1)) * D + d] : 0.f;
+        xv[ks] = a.x[(b * T + (tn - 1)) * D + (d < D ? d : D - 1)];
       }
     };
+    const auto gx_x = [&](float v) { return (lane & 15) < D ? v : 0.f; };   // x operand lanes d < D
     auto gx_fold = [&](int buf) {   // R of the tile folded next, from Zb[buf]
       if ((gxs % NT) == 0) {
 #pragma unroll
@@ -764,7 +767,7 @@ __global__ __launch_bounds__(SR_THREADS) void k_sweep_rows(Geom g, const bf16x8*
       for (int ks = 0; ks < 8; ++ks)
 #pragma unroll
         for (int h = 0; h < 2; ++h)
-          gx[0][h] = __builtin_amdgcn_mfma_f32_16x16x4f32(xcur[ks], Rq[4 * ks * 32 + 16 * h], gx[0][h], 0, 0, 0);
+          gx[0][h] = __builtin_amdgcn_mfma_f32_16x16x4f32(gx_x(xcur[ks]), Rq[4 * ks * 32 + 16 * h], gx[0][h], 0, 0, 0);
       const f32x4 r0 = gx[0][0], r1 = gx[0][1];
 #pragma unroll
       for (int k = 0; k + 1 < NT; ++k) {

@@ -21,7 +21,28 @@ import torch  # noqa: F401  (must precede the CDLL load, see module docstring)
 LIB_PATH = os.environ.get('ADMM_LSTM_LIB') or os.path.join(os.path.dirname(os.path.abspath(__file__)),
                                                           'libadmmlstm.so')
 
-ABI_VERSION = 2
+ABI_VERSION = 3
+
+# the sources whose sha256 the Makefile embeds in admm_build_info() (csrc/Makefile SRC_STAMP: SRC then HDR)
+_CSRC = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'csrc')
+_STAMP_FILES = ('admm_kernels.hip', 'admm_split3.hip', 'admm_host.hip', 'admm_dev.hpp', 'admm_kernels.hpp',
+                'admm_split3.hpp', os.path.join('..', '..', '..', 'include', 'admm_lstm.h'))
+
+
+def tree_stamp() -> str:
+    """The source stamp of the library sources in this tree (what a fresh build would embed)."""
+    import hashlib
+    h = hashlib.sha256()
+    for f in _STAMP_FILES:
+        with open(os.path.join(_CSRC, f), 'rb') as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
+def lib_stamp(lib=None) -> str:
+    """The source stamp the loaded library was built from (admm_build_info: '... src <stamp>')."""
+    info = (lib or load()).admm_build_info().decode()
+    return info.rsplit(' src ', 1)[1] if ' src ' in info else 'unstamped'
 VARIANT_ADMM, VARIANT_NO_DUAL_Y = 0, 1
 NCCL_UNIQUE_ID_BYTES = 128
 
@@ -80,6 +101,7 @@ _SIGNATURES = {
     'admm_step': (c_int, [c_void_p, c_void_p]),
     'admm_set_with_dual_y': (c_int, [c_void_p, c_int32]),
     'admm_invalidate_cache': (c_int, [c_void_p]),
+    'admm_ack_fault': (c_int, [c_void_p]),
     'admm_comm_unique_id': (c_int, [c_void_p, c_int64]),
     'admm_set_comm': (c_int, [c_void_p, c_void_p, c_int64, c_int, c_int]),
     'admm_set_comm_host': (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int]),

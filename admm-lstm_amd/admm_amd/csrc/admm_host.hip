@@ -175,7 +175,7 @@ struct AdmmCtx {
   int* status_host = nullptr;
   int* status_dev = nullptr;
   // hand-off timeouts already reported (admm_step refuses to run on a state a timed-out hand-off
-  // left invalid until the caller rewrites it: admm_bind, admm_init_state or admm_invalidate_cache)
+  // left invalid until the caller restores it and says so: admm_ack_fault, or admm_init_state)
   int handoff_ack = 0;
   // admm_debug_fault: one-shot fault injection (tests)
   bool fault_skip_publish = false, fault_capture = false;
@@ -556,8 +556,12 @@ extern "C" {
 
 int32_t admm_abi_version(void) { return ADMM_LSTM_ABI_VERSION; }
 
+#ifndef ADMM_SRC_STAMP
+#define ADMM_SRC_STAMP "unstamped"
+#endif
+// "... src <stamp>": the Makefile's hash of the sources this library was built from
 const char* admm_build_info(void) {
-  return "libadmmlstm gfx950 (fp32 MFMA v_mfma_f32_32x32x2_f32, RCCL), abi " "1";
+  return "libadmmlstm gfx950 (split bf16/fp16 and fp32 MFMA, RCCL), abi 3, src " ADMM_SRC_STAMP;
 }
 
 const char* admm_last_error(void) { return g_last_error.c_str(); }
@@ -724,7 +728,6 @@ int admm_bind(AdmmCtx* c, const AdmmBuffers* b) {
   c->buf = *b;
   c->bound = true;
   c->u_valid = false;
-  c->handoff_ack = c->status_host[2];
   c->z_valid = false;
   c->tgt_valid = false;
   c->gx_valid = false;
@@ -742,7 +745,6 @@ int admm_set_with_dual_y(AdmmCtx* c, int32_t flag) {
 
 int admm_invalidate_cache(AdmmCtx* c) {
   if (!c) return fail(ADMM_EINVAL, "NULL ctx");
-  c->handoff_ack = c->status_host[2];   // the caller rewrote state: a timed-out hand-off is behind it
   c->u_valid = false;
   c->z_valid = false;
   c->tgt_valid = false;
@@ -750,6 +752,12 @@ int admm_invalidate_cache(AdmmCtx* c) {
   c->lamh_known = false;
   c->range_valid = c->x1_valid = false;
   return ADMM_OK;
+}
+
+int admm_ack_fault(AdmmCtx* c) {
+  if (!c) return fail(ADMM_EINVAL, "NULL ctx");
+  c->handoff_ack = c->status_host[2];   // the caller restored the state: the timed-out hand-offs are behind it
+  return admm_invalidate_cache(c);
 }
 
 int admm_init_state(AdmmCtx* c, void* stream) {
@@ -853,11 +861,14 @@ int admm_step(AdmmCtx* c, void* stream) {
     const int hf = ((const volatile int*)c->status_host)[2];
     if (hf > c->handoff_ack)
       return fail(ADMM_EFAULT, "column-split sweep: %d hand-off wait(s) timed out in an earlier step; the state "
-                  "is invalid (restore it and call admm_invalidate_cache, or admm_init_state)", hf - c->handoff_ack);
+                  "is invalid (restore it and call admm_ack_fault, or admm_init_state)", hf - c->handoff_ack);
   }
   hipStream_t s = (hipStream_t)stream;
   DEVICE_GUARD(c->device);
   int rc;
+  // the column split's switch-off (stage_sweep) is decided here too: a replayed graph skips
+  // stage_sweep, and the flag is part of the signature, so the switch drops the graph at once
+  if (c->xbuf && !c->cs_off && ((const volatile int*)c->status_host)[3] >= kSweepFallbackLimit) c->cs_off = true;
   const StepSig sig = step_sig(c);
   const bool capturable = c->graph && !c->graph_disabled && !c->prof_mask && !c->host_ar;
   if (capturable && c->gexec && sig_eq(sig, c->gsig)) {

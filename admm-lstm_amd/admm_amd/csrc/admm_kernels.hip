@@ -406,9 +406,15 @@ __global__ __launch_bounds__(kThreads) void k_sweep_wt(int D, int H, int XC, Wei
 // leaves before touching the state, and the row-block sweep launched next does the work instead).
 constexpr unsigned kSweepPoison = 0x40000000u;
 constexpr uint64_t kSweepArriveTicks = 200000;   // 2 ms of the 100 MHz wall clock
-// A hand-off wait (exchange) that sees no tag t after this long gives up: 50 ms of the wall clock,
+// A hand-off wait (exchange) that sees no tag t for this long gives up: 50 ms of the wall clock,
 // against ~3 us per t in a healthy sweep.  The step is then invalid and counted (SweepT::fail).
+// Only time this wave was running counts: a gap between two polls longer than kHandoffGapTicks
+// (one poll takes ~1 us) means the dispatch was preempted or time-sliced -- the publishers were
+// paused too -- so the gap is not charged; and the wait must also have polled kHandoffMinSpins
+// times, so a few long gaps just under the bound cannot add up to a failure either.
 constexpr uint64_t kHandoffTicks = 5000000;
+constexpr uint64_t kHandoffGapTicks = 10000;     // 100 us
+constexpr unsigned kHandoffMinSpins = 20000;
 __device__ __forceinline__ bool sweep_arrive(unsigned* ctl, unsigned n) {
   unsigned v = __hip_atomic_fetch_add(ctl, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
   const uint64_t t0 = wall_clock64();
@@ -938,7 +944,7 @@ __global__ __launch_bounds__(SR_THREADS) void k_sweep_rows(Geom g, const bf16x8*
       return xo + (uint32_t)((hr * H + col) * 8);
     };
     const unsigned want = (unsigned)t;
-    uint64_t t0 = 0;
+    uint64_t prev = 0, waited = 0;
     for (unsigned spins = 0;; ++spins) {
       bool ok = true;
 #pragma unroll
@@ -949,9 +955,12 @@ __global__ __launch_bounds__(SR_THREADS) void k_sweep_rows(Geom g, const bf16x8*
 #pragma unroll
       for (int i = 0; i < NP; ++i) ok &= __float_as_uint(gv[i][1]) == want && __float_as_uint(gv[i][3]) == want;
       if (__all(ok)) break;
-      // bounded by the wall clock (the clock is read only once a wait is not immediately served)
-      if (spins == 0) t0 = wall_clock64();
-      else if (wall_clock64() - t0 > kHandoffTicks) {
+      // bounded by the wall clock this wave ran (the clock is read only once a wait is not
+      // immediately served; gaps from preemption are not charged, kHandoffGapTicks)
+      const uint64_t now = wall_clock64();
+      if (spins > 0 && now - prev < kHandoffGapTicks) waited += now - prev;
+      prev = now;
+      if (waited > kHandoffTicks && spins >= kHandoffMinSpins) {
         // a group did not publish h_t: the A image would hold stale h.  Counted per wave
         // (DevStats::handoff_fail); the host turns it into an error (admm_step / admm_get_stats)
         if (lane == 0 && a.fail) atomicAdd(a.fail, 1);
@@ -2017,8 +2026,8 @@ __device__ __forceinline__ T wave_sum_slots(T (&v)[N]) {   // in place: v is con
   return v[0];
 }
 
-// WT: written through (sc1) and drained by the storing wave, for a reader in another workgroup of the
-// same launch (the fused tail selection, tail_select_last)
+// WT: agent-scope stores for a reader in another workgroup of the same launch (the fused tail
+// selection, tail_select_last, which releases them)
 template <bool WT = false>
 __device__ __forceinline__ void trial_block_store(float (&acc)[kSlots], double* part, int q, int blk, int nblk) {
   __shared__ double red[4][kSlots];
@@ -2030,8 +2039,8 @@ __device__ __forceinline__ void trial_block_store(float (&acc)[kSlots], double* 
     const int k = threadIdx.x;
     const double v = (red[0][k] + red[1][k]) + (red[2][k] + red[3][k]);
     if constexpr (WT) {
+      // (released to agent scope by the same wave's fence in tail_select_last: all storing threads are wave 0)
       __hip_atomic_store(&part[((int64_t)q * kSlots + k) * nblk + blk], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     } else {
       part[((int64_t)q * kSlots + k) * nblk + blk] = v;
     }
@@ -2718,11 +2727,16 @@ __device__ __forceinline__ void tail_select_done(const TailSel& ts, int q) {
 }
 __device__ __forceinline__ void tail_select_last(const Geom& g, const TailSel& ts, int q, unsigned nblocks) {
   __shared__ int last_s;
-  __syncthreads();   // every storing wave has drained its write-through partials
-  if (threadIdx.x == 0)
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    // release: this workgroup's partials (stored by this wave, trial_block_store<true>) are visible at
+    // agent scope before its arrival counts; the last arriver acquires everyone's before reading them
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     last_s = __hip_atomic_fetch_add(&ts.count[q], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nblocks - 1;
+  }
   __syncthreads();
   if (!last_s) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   select_gate<true>(g, ts.hp, ts.a, q, 0, 1);
   if (threadIdx.x == 0) __hip_atomic_store(&ts.count[q], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }

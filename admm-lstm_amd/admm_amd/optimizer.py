@@ -361,7 +361,9 @@ class AdmmOptimizerBase(object):
         }
 
     def load_state_dict(self, state: dict) -> None:
-        """Copy a ``state_dict()`` into this optimizer's (bound) device tensors."""
+        """Copy a ``state_dict()`` into this optimizer's (bound) device tensors.  This is a
+        restore: it also acknowledges a column-split hand-off fault (``AdmmError`` code -6) that
+        left the previous state invalid (``acknowledge_fault``); restore the model's weights first."""
         shape = [self.batch_size, self.seq_len, self.input_size, self.hidden_size, self.output_size]
         if list(state.get('shape', [])) != shape:
             raise ValueError(f'checkpoint is for shape {state.get("shape")}, this optimizer has {shape}')
@@ -375,6 +377,13 @@ class AdmmOptimizerBase(object):
                         raise ValueError(f'checkpoint {part}[{k!r}] has shape {tuple(src[k].shape)}')
                     t.copy_(src[k].to(t.device, torch.float32))
         # gates['h'] changed version: the next step() rebuilds the z cache
+        self.acknowledge_fault()
+
+    def acknowledge_fault(self) -> None:
+        """Declare the bound state restored after a column-split hand-off fault (``admm_ack_fault``).
+        Until this (or ``load_state_dict``) is called, every ``step()`` raises ``AdmmError`` (code -6):
+        an in-place edit of the invalid state does not clear the fault."""
+        N.check(self._lib.admm_ack_fault(self._ctx), 'admm_ack_fault')
 
     def profile(self, classes=()) -> None:
         """Enable live hipEvent timing of the named kernel classes (``_native.PROF_CLASSES``)."""

@@ -171,16 +171,34 @@ CLASS_KERNELS = {'sweep': ('k_sweep_rows', 'k_sweep_t'), 'atr_h': ('k_atr3', 'k_
                  'resid': ('k_resid_gx', 'k_apply_dwx', 'k_resid<')}
 
 
-def pmc_traffic(cls: str, cfg_name: str):
-    """HBM bytes per launch of a kernel class from the newest committed PMC summary
-    (profiles/r*_pmc_<cfg>.json, written by tools/pmc_to_json.py from rocprofv3 FETCH_SIZE /
-    WRITE_SIZE passes of this same bench command), or None if there is none."""
+def counter_file(kind: str, cfg_name: str):
+    """(path, why) of the newest committed counter summary profiles/r*_<kind>_<cfg>.json (written by
+    tools/pmc_to_json.py) that measured THIS library: its lib_stamp must equal the source stamp the
+    loaded libadmmlstm.so was built from (admm_build_info).  path None: why says what is missing."""
     import glob
     import json
-    files = sorted(glob.glob(os.path.join(ROOT, 'profiles', f'r*_pmc_{cfg_name}.json')))
-    if not files or cls not in CLASS_KERNELS:
-        return None
-    kern = json.load(open(files[-1]))['kernels']
+    from admm_amd import _native as N
+    want = N.lib_stamp()
+    files = sorted(glob.glob(os.path.join(ROOT, 'profiles', f'r*_{kind}_{cfg_name}.json')))
+    for f in reversed(files):
+        if json.load(open(f)).get('lib_stamp') == want:
+            return f, None
+    return None, (f'no profiles/r*_{kind}_{cfg_name}.json measured this library (src {want}); '
+                  f'{len(files)} older summar{"y" if len(files) == 1 else "ies"} ignored')
+
+
+def pmc_traffic(cls: str, cfg_name: str):
+    """(HBM bytes per launch of a kernel class, source) from the newest committed PMC summary of this
+    library (counter_file: rocprofv3 FETCH_SIZE / WRITE_SIZE passes of this same bench command), or
+    (None, why)."""
+    import json
+    path, why = counter_file('pmc', cfg_name)
+    if path is None:
+        return None, why
+    src = os.path.relpath(path, ROOT)
+    if cls not in CLASS_KERNELS:
+        return None, f'{src}: no kernel family for class {cls}'
+    kern = json.load(open(path))['kernels']
     # trial passes after the first return early (gates already decided): use the full pass; the
     # column-split sweep is followed by its gated row-block launch, which exits at once: the max
     key = 'traffic_bytes_max' if cls in ('trial', 'trial_h', 'sweep') else 'traffic_bytes_median'
@@ -189,12 +207,12 @@ def pmc_traffic(cls: str, cfg_name: str):
         if vals:
             break
     if not vals:
-        return None
+        return None, f'{src}: no {cls} kernel in the summary'
     per = sum(vals) / len(vals)
     if cls == 'sweep' and prefix == 'k_sweep_t':   # per-t sweep: T time steps x 2 sample halves
         T = CONFIGS[cfg_name][1]
         per *= 2 * T
-    return per
+    return per, src
 
 
 # kernel families whose MFMA-busy fraction bench.py reports (SQ pass of tools/gpu.sh mfma:<cfg>)
@@ -203,20 +221,19 @@ MFMA_KERNELS = {'sweep': ('k_sweep_rows',), 'atr_h': ('k_atr3w<2, true>', 'k_atr
 
 
 def pmc_mfma_busy(cfg_name: str):
-    """Counted MFMA-busy fraction per kernel family from the newest committed SQ pass
-    (profiles/r*_sq_<cfg>.json, tools/gpu.sh mfma:<cfg>, tools/pmc_to_json.py --sq):
+    """Counted MFMA-busy fraction per kernel family from the newest committed SQ pass of this library
+    (counter_file: profiles/r*_sq_<cfg>.json, tools/gpu.sh mfma:<cfg>, tools/pmc_to_json.py --sq):
     SQ_VALU_MFMA_BUSY_CYCLES (cycles the matrix pipe of a SIMD is busy, summed over SIMDs) over
     4 SIMDs x SQ_BUSY_CU_CYCLES (the dispatch's busy cycles summed over CUs), i.e. the share of the
     kernel's time the matrix cores are issuing, against gfx950's MFMA peak issue rate.  Per dispatch,
     the largest over the family's dispatches (the gated row-block sweep launch after a column split
-    does no work).  None if there is no pass for this config."""
-    import glob
+    does no work).  {'source': None, 'why': ...} if no pass of this config measured this library."""
     import json
-    files = sorted(glob.glob(os.path.join(ROOT, 'profiles', f'r*_sq_{cfg_name}.json')))
-    if not files:
-        return None
-    kern = json.load(open(files[-1]))['kernels']
-    out = {'source': os.path.relpath(files[-1], ROOT)}
+    path, why = counter_file('sq', cfg_name)
+    if path is None:
+        return {'source': None, 'why': why}
+    kern = json.load(open(path))['kernels']
+    out = {'source': os.path.relpath(path, ROOT)}
     for cls, prefixes in MFMA_KERNELS.items():
         for prefix in prefixes:
             vals = [v['SQ_VALU_MFMA_BUSY_CYCLES_max'] / (4.0 * v['SQ_BUSY_CU_CYCLES_max'])
@@ -226,6 +243,25 @@ def pmc_mfma_busy(cfg_name: str):
                 out[cls] = round(max(vals), 4)
                 break
     return out
+
+
+def reference_loss(cfg_name: str, step: int, loss: float):
+    """The reference's training loss after ``step`` steps of this config's trajectory, where a committed
+    golden holds it (tests/golden/c3_25.npz: the reference's 25 steps of C3 = the default 5 warm-up + 20
+    timed steps, tests/golden/make_golden.py), beside this run's final loss: {step, loss, rel_diff}."""
+    import json
+    import numpy as np
+    if cfg_name != 'c3':
+        return None
+    path = os.path.join(ROOT, 'tests', 'golden', 'c3_25.npz')
+    if not os.path.exists(path):
+        return None
+    losses = json.loads(str(np.load(path, allow_pickle=False)['meta_json']))['losses']
+    if step >= len(losses):
+        return None
+    ref = losses[step]
+    return {'step': step, 'loss': ref, 'rel_diff': abs(loss - ref) / abs(ref), 'bar': 1e-5,
+            'source': 'tests/golden/c3_25.npz (the reference itself, tests/golden/make_golden.py)'}
 
 
 def host_cpu():
@@ -533,14 +569,15 @@ def main():
         roof['frac'] = roof['achieved'] / roof['peak']
         # traffic: measured HBM bytes per launch (PMC, DESIGN.md "Measurement"), next to the
         # algorithmic bytes per launch and the bytes this design moves
-        roof['traffic'] = pmc_traffic(cls, args.config)
+        roof['traffic'], roof['traffic_source'] = pmc_traffic(cls, args.config)
         roof['algorithmic_bytes'] = nbytes
         roof['design_bytes'] = design_bytes
         roof['algorithmic_flops'] = flops
         roof['mfma_frac_fp32'] = flops / avg_s / PEAK_FP32_MFMA    # SURVEY.md 8(d)'s MFMA fraction
         # the counted one (rocprofv3 SQ_VALU_MFMA_BUSY_CYCLES): matrix-pipe busy share of the kernel's time
         busy = pmc_mfma_busy(args.config)
-        roof['mfma_busy_frac'] = busy.get(cls) if busy else None
+        roof['mfma_busy_frac'] = busy.get(cls)
+        roof['mfma_busy_source'] = busy['source'] or busy['why']
         roof['mfma_busy'] = busy
         roof['kernel'] = cls
         roof['avg_launch_us'] = avg_s * 1e6
@@ -597,6 +634,7 @@ def main():
             'sweep': {'fallbacks': stats['sweep_fallbacks'], 'split_off': stats['sweep_split_off'],
                       'handoff_fail': stats['handoff_fail']},
             'final_train_mse': loss,
+            **({'reference_loss': ref} if (ref := reference_loss(args.config, args.warmup + args.steps, loss)) else {}),
         }
         print(json.dumps(out), flush=True)
     if dist is not None:

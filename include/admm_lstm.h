@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define ADMM_LSTM_ABI_VERSION 2
+#define ADMM_LSTM_ABI_VERSION 3
 
 enum {
   ADMM_OK = 0,
@@ -41,7 +41,7 @@ enum {
   ADMM_ESTATE = -5,   /* call not valid in the context's state (e.g. step before bind) */
   ADMM_EFAULT = -6    /* a step's device work failed an internal check (the column-split sweep's
                          hand-off timed out): the bound state is invalid until the caller rewrites
-                         it (admm_init_state, or a restore followed by admm_invalidate_cache) */
+                         it (admm_init_state, or a restore followed by admm_ack_fault) */
 };
 
 enum { ADMM_VARIANT_ADMM = 0, ADMM_VARIANT_NO_DUAL_Y = 1 };
@@ -142,6 +142,14 @@ int admm_set_with_dual_y(AdmmCtx* ctx, int32_t flag);
    outside admm_step to the weights, x, a gate plane or a dual plane (in particular the h dual
    at t < T, which would otherwise be read as zero); the next step then rebuilds them. */
 int admm_invalidate_cache(AdmmCtx* ctx);
+
+/* ABI 3.  Acknowledge the hand-off faults counted so far (AdmmStats::handoff_fail) after the
+   caller has restored the bound state (e.g. from a checkpoint): admm_step stops failing with
+   ADMM_EFAULT and the caches are invalidated as by admm_invalidate_cache.  Nothing else clears a
+   fault except admm_init_state (re-binding and cache invalidation do not): an in-place edit of
+   the invalid state is not a restore.  Replaces no reference interface (device faults have no
+   reference analogue). */
+int admm_ack_fault(AdmmCtx* ctx);
 
 /* Multi-GPU (one process per GPU): rank 0 calls admm_comm_unique_id, the bytes are
    broadcast out of band (torch.distributed), every rank calls admm_set_comm.  All batch

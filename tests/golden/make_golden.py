@@ -60,6 +60,10 @@ CASES = {
     # BASELINE configs at full size (compact: inputs as generator recipe + sha256, no state)
     'c3':           ('admm', False, 'uniform', 8192, 32, 16, 256, 5, False, 'GoogleStock'),
     'c5_1gpu':      ('no_dual_y', False, 'rw', 4096, 64, 1, 512, 3, False, 'GoogleStock'),
+    # the bench's own trajectory (bench.py default: 5 warm-up + 20 timed steps = steps 1..25 of C3), and the
+    # same capture on 4 threads (a different reduction order) as the reference's own noise floor
+    'c3_25':        ('admm', False, 'uniform', 8192, 32, 16, 256, 25, False, 'GoogleStock'),
+    'c3_25_t4':     ('admm', False, 'uniform', 8192, 32, 16, 256, 25, False, 'GoogleStock'),
     # C4's global problem (65536 samples; the 8-GPU run shards exactly this) on one device
     'c4g':          ('admm', False, 'uniform', 65536, 32, 16, 256, 3, False, 'GoogleStock'),
     # perturbed starting state (golden_io.perturb_state: 1e-2 noise on gates and duals), so that the
@@ -76,6 +80,8 @@ CASES = {
 # once by the fp64 oracle (oracle.admm_oracle.fp64_decisions) to record how the reference's
 # fp32 line-search decisions compare with fp64 ones from the same state
 COMPACT = {'c3': {'full_w': (1, 2, 3, 4, 5), 'fp64': True},
+           'c3_25': {'full_w': (5, 10, 15, 20, 25), 'fp64': False},
+           'c3_25_t4': {'full_w': (25,), 'fp64': False},
            'c5_1gpu': {'full_w': (3,), 'fp64': False},
            'c4g': {'full_w': (3,), 'fp64': False},
            't4_pert_h256': {'full_w': (1, 2, 3), 'fp64': True},
@@ -85,6 +91,8 @@ COMPACT = {'c3': {'full_w': (1, 2, 3, 4, 5), 'fp64': True},
 PERTURB = {'t4_pert_h256': {'seed': 11, 'scale': 1e-2}, 't4_pert_h512': {'seed': 11, 'scale': 1e-2},
            't32_pert_h256': {'seed': 11, 'scale': 1e-2}}
 WSTRIDE = 16
+# torch CPU threads per case (default: whatever torch picks, 8 in this container)
+THREADS = {'c3_25': 8, 'c3_25_t4': 4}
 
 
 def goog_windows():
@@ -165,6 +173,8 @@ def split_searches(log, fn_name):
 def run_case(name):
     variant, dual_y, gen, B, T, D, H, steps, full, pset = CASES[name]
     os.chdir('/tmp')
+    if name in THREADS:
+        torch.set_num_threads(THREADS[name])
     if REF not in sys.path:
         sys.path.insert(0, REF)
     import admm as ref_admm

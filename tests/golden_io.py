@@ -128,8 +128,11 @@ _NAMES = sorted(f[:-4] for f in os.listdir(GOLDEN) if f.endswith('.npz') and not
 # tests/test_gpu_weight_phase.py runs them
 PERTURBED = [n for n in _NAMES if Golden(n).meta.get('perturb')]
 COMPACT = [n for n in _NAMES if Golden(n).compact and n not in PERTURBED]
+# long full-size trajectories (the bench's own 25 steps of C3, captured at two thread counts):
+# tests/test_gpu_trajectory.py runs them
+LONG = [n for n in COMPACT if Golden(n).meta['steps'] >= 20]
 # full-size fixtures the reference itself produced, and those the oracle produced (c5g)
-COMPACT_REF = [n for n in COMPACT if Golden(n).source == 'reference']
-COMPACT_ORACLE = [n for n in COMPACT if Golden(n).source == 'oracle']
+COMPACT_REF = [n for n in COMPACT if Golden(n).source == 'reference' and n not in LONG]
+COMPACT_ORACLE = [n for n in COMPACT if Golden(n).source == 'oracle' and n not in LONG]
 ALL = [n for n in _NAMES if n not in COMPACT and n not in PERTURBED]
 FULL = [n for n in ALL if Golden(n).full_state]

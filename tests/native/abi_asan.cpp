@@ -85,6 +85,7 @@ static void check_args() {
   CHECK(admm_step(nullptr, nullptr) == ADMM_EINVAL);
   CHECK(admm_set_with_dual_y(nullptr, 1) == ADMM_EINVAL);
   CHECK(admm_invalidate_cache(nullptr) == ADMM_EINVAL);
+  CHECK(admm_ack_fault(nullptr) == ADMM_EINVAL);
   AdmmStats st;
   CHECK(admm_get_stats(nullptr, &st) != ADMM_OK);
   int32_t u = 0, nf = 0;
@@ -242,6 +243,7 @@ static void run_context(int64_t B, int T, int D, int H, int O, int variant, int 
   CHECK(admm_poll_faults(ctx, nullptr, &fb) == ADMM_EINVAL);
   CHECK(st.handoff_fail == 0 && st.graph_disabled == 0);
   CHECK(admm_debug_fault(ctx, 0) == ADMM_OK);
+  CHECK(admm_ack_fault(ctx) == ADMM_OK);   // nothing to acknowledge: invalidates the caches only
   CHECK(admm_debug_fault(ctx, 7) == ADMM_EINVAL);
   // z cache copy-out: too small a destination is refused, the right size is accepted
   const int64_t zbytes = (int64_t)4 * B * T * H * 4;

@@ -1016,8 +1016,9 @@ def test_column_split_handoff_timeout_is_an_error(mods, dev):
     (ADVICE r4).  admm_debug_fault(1) makes row block 0's column group 1 skip its
     publish of h_1 in the next step: the other groups' waits time out (50 ms of the wall clock),
     the step counts it in AdmmStats::handoff_fail, admm_poll_status returns ADMM_EFAULT, and the
-    next step() raises AdmmError (code -6) instead of stepping on the invalid state.  Restoring the
-    state and invalidating the caches clears it: the step after that runs and the count stays put."""
+    next step() raises AdmmError (code -6) instead of stepping on the invalid state.  An in-place
+    edit of the state (which invalidates the caches) does not clear it; restoring the
+    state with load_state_dict does: the step after that runs and the count stays put."""
     from blocks.lstm import LSTM
     from parameters import example_parameter_dictionary
     from admm_amd import _native as N
@@ -1033,7 +1034,7 @@ def test_column_split_handoff_timeout_is_an_error(mods, dev):
     lib = N.load()
     opt.step()
     assert opt.last_step_stats()['handoff_fail'] == 0
-    snap = {k: v.clone() for k, v in opt.gates.items()}, {k: v.clone() for k, v in opt.duals.items()}
+    snap = opt.state_dict()
     wsnap = [p.detach().clone() for p in m.parameters()]
     if lib.admm_debug_fault(opt._ctx, 1) != 0:
         pytest.skip('no column-split sweep on this device (fewer than 256 CUs)')
@@ -1045,14 +1046,17 @@ def test_column_split_handoff_timeout_is_an_error(mods, dev):
     with pytest.raises(N.AdmmError) as ei:
         opt.step()
     assert ei.value.code == N.EFAULT and 'hand-off' in str(ei.value)
-    # restore the pre-fault state (as from a checkpoint) and invalidate: stepping works again
+    # an in-place edit invalidates the caches but is not a restore: still refused
     with torch.no_grad():
-        for k, v in snap[0].items():
-            opt.gates[k].copy_(v)
-        for k, v in snap[1].items():
-            opt.duals[k].copy_(v)
+        opt.gates['h'].mul_(1.0)
+    with pytest.raises(N.AdmmError) as ei:
+        opt.step()
+    assert ei.value.code == N.EFAULT
+    # restore the pre-fault state (as from a checkpoint): stepping works again
+    with torch.no_grad():
         for p, v in zip(m.parameters(), wsnap):
             p.copy_(v)
+    opt.load_state_dict(snap)
     opt.step()
     st2 = opt.last_step_stats()
     assert st2['handoff_fail'] == st['handoff_fail'] and st2['nonfinite'] == 0, st2

@@ -8,7 +8,7 @@ operands, and the full primal/dual state.
 import pytest
 import torch
 
-from golden_io import (ALL, COMPACT_ORACLE, COMPACT_REF, FULL, GATES6, PERTURBED, WEIGHT_NAMES, Golden,
+from golden_io import (ALL, COMPACT_ORACLE, COMPACT_REF, FULL, GATES6, LONG, PERTURBED, WEIGHT_NAMES, Golden,
                        perturb_state)
 from oracle import admm_oracle as O
 
@@ -118,7 +118,24 @@ def test_fixture_sources():
     case (test_gpu_fullsize.test_fullsize_matches_oracle_fixture)."""
     assert COMPACT_ORACLE == ['c5g']
     assert set(COMPACT_REF) == {'c3', 'c5_1gpu', 'c4g'}
-    for n in ALL + PERTURBED + COMPACT_REF:
+    assert set(LONG) == {'c3_25', 'c3_25_t4'}
+    for n in ALL + PERTURBED + COMPACT_REF + LONG:
         g = Golden(n)
         assert g.source == 'reference', n
         assert g.meta.get('generator', 'tests/golden/make_golden.py').startswith('tests/golden/make_golden.py'), n
+
+
+def test_long_capture_reproduces_c3():
+    """The 25-step capture of the bench's trajectory (c3_25) repeats the 5-step c3 capture bit for bit over
+    their common steps (both the reference on 8 threads in this container): same losses, exponents and
+    weights.  c3_25_t4 (4 threads) is the reference's own spread, compared in tests/test_gpu_trajectory.py."""
+    g25, g5 = Golden('c3_25'), Golden('c3')
+    assert g25.threads == g5.threads == 8 and Golden('c3_25_t4').threads == 4
+    assert g25.compact['x_sha256'] == g5.compact['x_sha256'] and g25.compact['y_sha256'] == g5.compact['y_sha256']
+    assert g25.losses[:6] == g5.losses
+    for s in range(1, 6):
+        assert g25.ks(s) == g5.ks(s), s
+        for k in WEIGHT_NAMES:
+            a, b = g25.t(f'w{s}_{k}'), g5.t(f'w{s}_{k}')
+            if a.shape == b.shape:
+                assert torch.equal(a, b), (s, k)

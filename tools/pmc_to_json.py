@@ -22,6 +22,22 @@ import re
 import statistics
 import sys
 
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def lib_stamp():
+    """Source stamp of the library the profiled bench loaded (ADMM_LSTM_LIB or the in-tree build):
+    bench.py takes counters only from summaries whose stamp equals its own library's."""
+    import ctypes
+    path = os.environ.get('ADMM_LSTM_LIB') or os.path.join(ROOT, 'admm-lstm_amd', 'admm_amd', 'libadmmlstm.so')
+    try:
+        fn = ctypes.CDLL(path).admm_build_info
+        fn.restype = ctypes.c_char_p
+        info = fn().decode()
+    except (OSError, AttributeError):
+        return 'unknown'
+    return info.rsplit(' src ', 1)[1] if ' src ' in info else 'unstamped'
+
 
 def _rows(d):
     for f in glob.glob(os.path.join(d, '**', '*counter_collection.csv'), recursive=True):
@@ -41,7 +57,7 @@ def _load(d):
 def main(fetch_dir, write_dir, out_path, note=''):
     fetch, write = _load(fetch_dir), _load(write_dir)
     res = {'note': note, 'units': 'bytes per dispatch', 'correction': 'read = 2 x FETCH_SIZE (gfx950)',
-           'kernels': {}}
+           'lib_stamp': lib_stamp(), 'kernels': {}}
     for k in sorted(fetch):
         f, w = fetch[k], write.get(k, [0.0])
         res['kernels'][k] = {
@@ -63,7 +79,7 @@ def main_sq(run_dir, out_path, note=''):
     for (k, _disp, c), v in acc.items():
         per[k][c].append(v)
     res = {'note': note, 'units': 'counter value per dispatch (SQ cycles as rocprofv3 reports them)',
-           'kernels': {}}
+           'lib_stamp': lib_stamp(), 'kernels': {}}
     for k in sorted(per):
         ent = {'dispatches': max(len(v) for v in per[k].values())}
         for c, vals in sorted(per[k].items()):

@@ -18,6 +18,7 @@ Two runs through the C ABI, per step:
 Set ``ADMM_PARITY_OUT=<dir>`` for a JSON record per run (``parity_c3_25_{free,forced}.json``).
 """
 import ctypes
+import functools
 import json
 import os
 
@@ -46,6 +47,11 @@ def mods():
     return _load_mods()
 
 
+@functools.lru_cache(maxsize=None)
+def _golden(name):
+    return Golden(name)
+
+
 def _rel_wdiff(got, want):
     return float((got - want).abs().max()) / max(float(want.abs().max()), 1e-30)
 
@@ -61,7 +67,7 @@ def _compare(g, s, name, got):
 def ref_spread(s):
     """The reference's own 8- vs 4-thread spread at step s: loss (relative) and the largest weight
     difference relative to the weight's largest entry (over the entries both captures keep)."""
-    g8, g4 = Golden('c3_25'), Golden('c3_25_t4')
+    g8, g4 = _golden('c3_25'), _golden('c3_25_t4')
     loss = abs(g8.losses[s] - g4.losses[s]) / abs(g8.losses[s])
     w = 0.0
     for n in ('x2i', 'h2i', 'x2f', 'h2f', 'x2g', 'h2g', 'x2o', 'h2o', 'out'):
@@ -76,7 +82,7 @@ def ref_spread(s):
 
 def _trajectory(mods, dev, force: bool):
     from admm_amd import _native as N
-    g = Golden('c3_25')
+    g = _golden('c3_25')
     model, opt = _optimizer(g, mods, dev)
     x, y = g.x.to(dev), g.y.to(dev)
     lib = opt._lib
@@ -101,7 +107,7 @@ def _trajectory(mods, dev, force: bool):
         loss = _loss(model, x, y)
         wd = {n: _compare(g, s, n, p.detach().cpu()) for n, p in model.named_parameters()}
         sl, sw = ref_spread(s)
-        recs.append({'step': s, 'loss': loss, 'ref_loss': g.losses[s], 'ref4_loss': Golden('c3_25_t4').losses[s],
+        recs.append({'step': s, 'loss': loss, 'ref_loss': g.losses[s], 'ref4_loss': _golden('c3_25_t4').losses[s],
                      'loss_rel': abs(loss - g.losses[s]) / abs(g.losses[s]), 'ref_spread_loss': sl,
                      'wdiff_max': max(wd.values()), 'wdiff': wd, 'ref_spread_w': sw,
                      'k': ks, 'ref_k': ref_k, 'own_k': own, 'theta_h': st['theta_h']})

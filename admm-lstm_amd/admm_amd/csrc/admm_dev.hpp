@@ -119,7 +119,34 @@ __device__ __forceinline__ float div_fast(float a, float b) {
   return fmaf(fmaf(-b, q, a), r, q);
 }
 
-// phi(z) and phi'(z) for the gradient / residual / line-search paths, from one v_exp and one
+// sigma(z) for the sweep (and the h-side gradient's residual): accurate expf, 1/(1+e) by v_rcp and one
+// Newton step (div_fast)
+__device__ __forceinline__ SigPair sig_sweep2(float z) {   // sigma(z) and 1 - sigma(z) without cancellation
+  const float e = expf(-fabsf(z));
+  const float r = div_fast(1.f, 1.f + e);
+  const float er = e * r;
+  return z >= 0.f ? SigPair{r, er} : SigPair{er, r};
+}
+
+// phi(z) and phi'(z) of the h-side gradient's residual R = (phi(z) - tgt) phi'(z) (admm.py:302-312): the
+// stored gates' activation (sig_pair / tanhf, as k_forward_t and k_resid_gx; ~1 ulp).  phi(z) - tgt is a
+// difference of O(1) numbers that agree to ~1e-7 at C3, so phi's rounding is most of G (DESIGN.md
+// section 2): with phi_fast's few ulps here the weights of the bench's 25 forced steps drifted 7x
+// further from the fp64 trajectory than the reference's own (round 6); and where
+// the stored h-side state is phi(z) itself (step 1) this activation gives R = 0 exactly, as the reference
+template <bool TANH>
+__device__ __forceinline__ void phi_acc(float z, float& phi, float& dphi) {
+  if (TANH) {
+    phi = tanhf(z);
+    dphi = 1.f - phi * phi;
+  } else {
+    const SigPair sp = sig_pair(z);
+    phi = sp.s;
+    dphi = sp.s * sp.sc;
+  }
+}
+
+// phi(z) and phi'(z) for the line-search paths (decisions only), from one v_exp and one
 // v_rcp (a few ulp; these feed sums, not the stored state).  With w = |z| (sigmoid) or 2|z|
 // (tanh), E = exp(-w), r = 1/(1+E):  sigma: phi = r or E r, phi' = E r^2;  tanh: |phi| =
 // -expm1(-w) r (no cancellation near 0), phi' = 4 E r^2.

@@ -159,13 +159,6 @@ struct SweepIn {
   float f0, g0, c0, h0, cp;   // old f, g, c, h at t; new c at t-1
   float li, lf, lg, lo, lc, lh;
 };
-// sigma(z) for the sweep: accurate expf, 1/(1+e) by v_rcp and one Newton step (div_fast)
-__device__ __forceinline__ SigPair sig_sweep2(float z) {   // sigma(z) and 1 - sigma(z) without cancellation
-  const float e = expf(-fabsf(z));
-  const float r = div_fast(1.f, 1.f + e);
-  const float er = e * r;
-  return z >= 0.f ? SigPair{r, er} : SigPair{er, r};
-}
 struct SweepRes {
   float i1, f1, g1, o1, c1, h1;
   float li, lf, lg, lo, lc;
@@ -1437,7 +1430,7 @@ struct AtRFusedSrc {
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       float phi, dphi;
-      phi_fast<TANH>(zz[u], phi, dphi);
+      phi_acc<TANH>(zz[u], phi, dphi);
       r[u] = (phi - tt[u]) * dphi;
     }
     return make_float4(r[0], r[1], r[2], r[3]);
@@ -3793,8 +3786,8 @@ void launch_trial_debug(int64_t n, int tanh_gate, int kbase, const float* z, con
 // stage, element by element with the activation of the kernel that formed it there (the
 // admm.py:302-312 residual), so a test can recompute G = rho A^T R on identical operands.
 //   mode 0: the persistent sweep's (sweep_point: sig_sweep2 / tanhf; the x stage's G_x partials)
-//   mode 1: k_resid_gx's (sig_pair / tanhf, the stored gates' activation)
-//   mode 2: phi_fast (the h stage's k_atr3w / k_atr_fused staging)
+//   mode 1: phi_acc (sig_pair / tanhf, the stored gates' activation): k_resid_gx's, and the h stage's
+//           k_atr3w / k_atr_fused staging
 template <int MODE>
 __global__ __launch_bounds__(kThreads) void k_debug_resid(int64_t n, const float* __restrict__ z,
                                                            const float* __restrict__ tgt, float* __restrict__ R) {
@@ -3802,14 +3795,14 @@ __global__ __launch_bounds__(kThreads) void k_debug_resid(int64_t n, const float
     const bool th = i / n == 2;
     const float zz = z[i], tt = tgt[i];
     float phi, dphi;
-    if (MODE == 2) {
-      if (th) phi_fast<true>(zz, phi, dphi);
-      else phi_fast<false>(zz, phi, dphi);
+    if (MODE == 1) {
+      if (th) phi_acc<true>(zz, phi, dphi);
+      else phi_acc<false>(zz, phi, dphi);
     } else if (th) {
       phi = tanhf(zz);
       dphi = 1.f - phi * phi;
     } else {
-      const SigPair sp = MODE == 0 ? sig_sweep2(zz) : sig_pair(zz);
+      const SigPair sp = sig_sweep2(zz);
       phi = sp.s;
       dphi = sp.s * sp.sc;
     }
@@ -3820,9 +3813,8 @@ __global__ __launch_bounds__(kThreads) void k_debug_resid(int64_t n, const float
 void launch_debug_resid(const Geom& g, int mode, const float* z, const float* tgt, float* R, hipStream_t s) {
   const int64_t n = g.BT() * g.H;
   const int nb = (int)std::min<int64_t>((4 * n + kThreads - 1) / kThreads, 8192);
-  if (mode == 0) k_debug_resid<0><<<nb, kThreads, 0, s>>>(n, z, tgt, R);
-  else if (mode == 1) k_debug_resid<1><<<nb, kThreads, 0, s>>>(n, z, tgt, R);
-  else k_debug_resid<2><<<nb, kThreads, 0, s>>>(n, z, tgt, R);
+  if (mode == 1) k_debug_resid<1><<<nb, kThreads, 0, s>>>(n, z, tgt, R);
+  else k_debug_resid<0><<<nb, kThreads, 0, s>>>(n, z, tgt, R);
 }
 
 void launch_trial_reduce(const Geom& g, int pass, const double* part, int nblk, const int* found, double* sums,

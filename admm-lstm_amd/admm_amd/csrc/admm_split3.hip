@@ -256,6 +256,7 @@ __device__ __forceinline__ int a3_off(int row, int col) {   // bf16 offset of (r
 // each operand per step (one 1-KB row per wave-instruction), two steps ahead through a two-slot
 // register ring.
 constexpr int A3W_THREADS = 512;
+
 #ifndef A3W_ABL
 #define A3W_ABL 0   // timing ablations for tools/build_lib_variant.sh: 1 no loads, 2 no MFMAs
 #endif
@@ -377,7 +378,7 @@ __device__ __forceinline__ void atr3w_body(const Geom& g, int q, int sp, int nsp
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
         float phi, dphi;
-        phi_fast<TANH>(zz[u], phi, dphi);
+        phi_acc<TANH>(zz[u], phi, dphi);
         rv[u] = ok ? (phi - tt[u]) * dphi : 0.f;
       }
       if constexpr (F16) pieces(rv * scl.y);

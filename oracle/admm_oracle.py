@@ -184,6 +184,11 @@ class Stepper:
         self.hp = hyper
         self.comm = comm or _LocalComm()
         self.trace_fw = trace_fw  # also record f(W) per search (one extra objective pass; off when timing)
+        # (k8, ht_fails) or None: replay given line-search outcomes instead of searching -- the eight
+        # exponents in step order (x2i, h2i, x2f, ...) and the number of failing h_T tests, i.e. the
+        # theta the reference's loops end with (admm.py:331-343, 474-482); the library's twin is
+        # admm_debug_force.  Set before each step() (tests/test_gpu_trajectory.py)
+        self.force = None
 
     # -- accessors that copy, like the reference's getters (admm.py:187-222)
     def _slice(self, store, q, t):
@@ -280,7 +285,7 @@ class Stepper:
         theta = 1
         trial = w + grad / theta
         tests = []
-        while True:
+        while self.force is None:
             fb, e = f(trial), est(trial, theta)
             worse = bool(fb > e)
             tests.append((float(fb), float(e), worse))
@@ -288,10 +293,14 @@ class Stepper:
                 break
             theta *= 2
             trial = w + grad / theta
+        k = len(tests) - 1
+        if self.force is not None:   # the loop above would have ended at theta = 2^k
+            k = self.force[0][2 * GATES4.index(q) + (side == 'h')]
+            theta = 2 ** k
         theta /= 2
         bq = self.hp.beta[name].clone().detach()
         st.W[name] = (0.5 * rq * T * theta * w - grad) / (bq + 0.5 * rq * theta * T)
-        rec = {'name': name, 'k': len(tests) - 1, 'tests': tests}
+        rec = {'name': name, 'k': k, 'tests': tests}
         if self.trace_fw:
             rec['f_w'] = float(f(w))
             rec['grad'] = grad
@@ -377,7 +386,9 @@ class Stepper:
         theta, cap = 0.1, 1
         trial = point(theta)
         tests = []
-        while True:
+        if self.force is not None:   # the loop below doubles theta once per failing test
+            theta = 0.1 * 2 ** self.force[1]
+        while self.force is None:
             fb, e = f(trial), est(trial, theta)
             worse = bool(fb > e)
             tests.append((float(fb), float(e), worse))

@@ -12,8 +12,17 @@ Two runs through the C ABI, per step:
   must stay within 1e-5 relative of the reference's at every one of the 25 steps (north_star's bar).
 * **forced**: the library replays the reference's recorded decisions (``admm_debug_force``: its eight
   exponents and its h_T search per step) while still running every search itself.  What is left is
-  the arithmetic alone (the closed forms, the split-product GEMMs, the sweep), so the weight drift of
-  this run is compared with the reference's own spread between its two captures.
+  the arithmetic alone (the closed forms, the split-product GEMMs, the sweep).  The loss must again stay
+  within 1e-5 at every step.  The weights drift from the reference's by more than the reference's own
+  8-vs-4-thread spread (1e-7): at C3 the gradient G is largely the fp32 rounding of phi(z) - tgt
+  (DESIGN.md section 2), and the updates G / (rho theta T / 2) grow to ~7e-6 of W per step by step
+  25, so any other fp32 arithmetic moves the weights apart by a share of the updates themselves,
+  while the two reference captures differ only in the GEMMs' summation order.  The bar is therefore
+  the exact trajectory: the same 25 forced steps by the oracle in fp64 (and in fp32 on the GPU's
+  torch ops, another fp32 platform, recorded beside it).  The library must be at most 2x as far from
+  the fp64 weights as the reference itself is, and at most 2x as far from the reference's weights as the
+  GPU-side fp32 oracle is, at every step (round 6: with the h-side gradient's residual on the stored
+  gates' activation instead of phi_fast).
 
 Set ``ADMM_PARITY_OUT=<dir>`` for a JSON record per run (``parity_c3_25_{free,forced}.json``).
 """
@@ -30,10 +39,11 @@ from test_gpu_parity import LOSS_RTOL, _loss, _optimizer
 
 pytestmark = pytest.mark.gpu
 
-# the forced run's weights may drift from the reference by at most this many times the reference's own
-# 8-vs-4-thread spread at the same step (and the spread floor below, where the two captures agree exactly)
-DRIFT_VS_SPREAD = 4.0
-SPREAD_FLOOR = 1e-7
+# the forced run's weights may be at most this many times as far from the fp64 trajectory as the
+# reference's own weights are, and from the reference's weights as the GPU fp32 oracle's are (plus the
+# floor, where they agree to fp32 resolution)
+DRIFT_VS_REF = 2.0
+DRIFT_FLOOR = 2e-7
 
 
 @pytest.fixture(scope='module')
@@ -80,7 +90,34 @@ def ref_spread(s):
     return loss, w
 
 
-def _trajectory(mods, dev, force: bool):
+def _keep(g, s, name, w):
+    """The entries of a full weight the fixture keeps at step s (every wstride-th of h2q at compact steps)."""
+    if not g.full_weights(s) and name.startswith('h2'):
+        return w.reshape(-1)[::g.compact['wstride']]
+    return w
+
+
+def _oracle_forced(dtype, dev):
+    """The oracle (the reference's op structure) on the GPU's torch ops in dtype, replaying the reference's
+    decisions (Stepper.force): the exact trajectory (fp64) and another fp32 platform (fp32).  Returns the
+    weights after each step as CPU fp64 tensors."""
+    from oracle import admm_oracle as O
+    g = _golden('c3_25')
+    torch.manual_seed(0)
+    W = {k: v.to(dev, dtype) for k, v in O.init_weights(g.D, g.H, g.O).items()}
+    st = O.init_state(g.x.to(dev, dtype), g.y.to(dev, dtype), W)
+    stp = O.Stepper(O.Hyper.from_dict(g.params, g.variant, g.with_dual_y).cast(dtype))
+    out = []
+    for s in range(1, g.steps + 1):
+        stp.force = (g.ks(s), sum(1 for _, _, r in g.searches[s - 1]['hT'] if r))
+        stp.step(st)
+        out.append({k: v.detach().to('cpu', torch.float64) for k, v in st.W.items()})
+    del st
+    torch.cuda.empty_cache()
+    return out
+
+
+def _trajectory(mods, dev, force: bool, keep_weights: bool = False):
     from admm_amd import _native as N
     g = _golden('c3_25')
     model, opt = _optimizer(g, mods, dev)
@@ -111,16 +148,23 @@ def _trajectory(mods, dev, force: bool):
                      'loss_rel': abs(loss - g.losses[s]) / abs(g.losses[s]), 'ref_spread_loss': sl,
                      'wdiff_max': max(wd.values()), 'wdiff': wd, 'ref_spread_w': sw,
                      'k': ks, 'ref_k': ref_k, 'own_k': own, 'theta_h': st['theta_h']})
+        if keep_weights:
+            recs[-1]['W'] = {n: p.detach().to('cpu', torch.float64) for n, p in model.named_parameters()}
     if force:
         N.check(lib.admm_debug_force(opt._ctx, None, 0), 'admm_debug_force')
     del opt, model
     torch.cuda.empty_cache()
+    if not force:
+        _write('free', recs)
+    return recs
+
+
+def _write(run, recs):
     out = os.environ.get('ADMM_PARITY_OUT')
     if out:
         os.makedirs(out, exist_ok=True)
-        with open(os.path.join(out, f'parity_c3_25_{"forced" if force else "free"}.json'), 'w') as f:
-            json.dump({'steps': recs}, f, indent=1)
-    return recs
+        with open(os.path.join(out, f'parity_c3_25_{run}.json'), 'w') as f:
+            json.dump({'steps': [{k: v for k, v in r.items() if k != 'W'} for r in recs]}, f, indent=1)
 
 
 def test_bench_trajectory_free_run(mods, dev):
@@ -133,10 +177,23 @@ def test_bench_trajectory_free_run(mods, dev):
 
 def test_bench_trajectory_forced_decisions(mods, dev):
     """The same 25 steps replaying the reference's decisions: the loss within 1e-5 at every step, and the
-    weight drift (arithmetic alone) within DRIFT_VS_SPREAD x the reference's own thread-count spread."""
-    recs = _trajectory(mods, dev, force=True)
+    library's weights at most DRIFT_VS_REF x as far from the exact (fp64) trajectory as the reference's."""
+    recs = _trajectory(mods, dev, force=True, keep_weights=True)
+    w64 = _oracle_forced(torch.float64, dev)
+    w32 = _oracle_forced(torch.float32, dev)
+    g = _golden('c3_25')
+    for r, e64, e32 in zip(recs, w64, w32):
+        s = r['step']
+        lib64 = ref64 = gpu32ref = 0.0
+        for n in r['W']:
+            ref = g.t(f'w{s}_{n}').double()
+            lib64 = max(lib64, _rel_wdiff(_keep(g, s, n, r['W'][n]), _keep(g, s, n, e64[n])))
+            ref64 = max(ref64, _rel_wdiff(ref, _keep(g, s, n, e64[n])))
+            gpu32ref = max(gpu32ref, _rel_wdiff(_keep(g, s, n, e32[n]), ref))
+        r.update({'lib_vs_fp64': lib64, 'ref_vs_fp64': ref64, 'gpu32_oracle_vs_ref': gpu32ref})
+    _write('forced', recs)
     for r in recs:
         assert r['loss_rel'] <= LOSS_RTOL, (r['step'], r['loss'], r['ref_loss'])
-        bound = DRIFT_VS_SPREAD * max(r['ref_spread_w'], SPREAD_FLOOR)
-        assert r['wdiff_max'] <= bound, (r['step'], r['wdiff_max'], r['ref_spread_w'],
-                                         [(q['step'], q['wdiff_max'], q['ref_spread_w']) for q in recs])
+        table = [(q['step'], q['lib_vs_fp64'], q['ref_vs_fp64'], q['wdiff_max'], q['gpu32_oracle_vs_ref']) for q in recs]
+        assert r['lib_vs_fp64'] <= DRIFT_VS_REF * r['ref_vs_fp64'] + DRIFT_FLOOR, table
+        assert r['wdiff_max'] <= DRIFT_VS_REF * r['gpu32_oracle_vs_ref'] + DRIFT_FLOOR, table

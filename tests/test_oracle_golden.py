@@ -139,3 +139,22 @@ def test_long_capture_reproduces_c3():
             a, b = g25.t(f'w{s}_{k}'), g5.t(f'w{s}_{k}')
             if a.shape == b.shape:
                 assert torch.equal(a, b), (s, k)
+
+
+@pytest.mark.parametrize('name', ['t0_admm', 't0_nodualy', 't2_c2'])
+def test_forced_replay_bit_exact(name):
+    """Stepper.force (replay given line-search outcomes instead of searching; the oracle's twin of the
+    library's admm_debug_force) with the reference's own recorded outcomes reproduces the reference
+    bit for bit: the searches only pick theta, and forcing sets the theta their loops ended with."""
+    g = Golden(name)
+    torch.manual_seed(0)
+    W = O.init_weights(g.D, g.H, g.O)
+    st = O.init_state(g.x, g.y, W)
+    stp = O.Stepper(O.Hyper.from_dict(g.params, g.variant, g.with_dual_y))
+    for s in range(1, min(g.steps, 4) + 1):
+        stp.force = (g.ks(s), sum(1 for _, _, r in g.searches[s - 1]['hT'] if r))
+        rec = stp.step(st)
+        assert [r['k'] for r in rec['weights']] == g.ks(s) and all(not r['tests'] for r in rec['weights'])
+        for k in WEIGHT_NAMES:
+            assert torch.equal(st.W[k], g.t(f'w{s}_{k}')), (s, k)
+        assert O.mse(g.x, g.y, st.W) == g.losses[s]

@@ -43,9 +43,14 @@ struct SigPair {
   float sc;  // 1 - sigma(z), computed without cancellation
 };
 
+__device__ __forceinline__ float div_fast(float a, float b);
+// sigma(z) and 1 - sigma(z) without cancellation: accurate expf, then 1 / (1 + e) by v_rcp and one Newton
+// step (div_fast), which equals the IEEE quotient 1.f / (1 + e) for every float 1 + e in [1, 2]: the pair
+// is bit-identical to the expf + IEEE-division form over all finite z (tools/sigcheck.hip, exhaustive on
+// an MI355X: profiles/r06f_sigcheck.txt) at half its VALU
 __device__ __forceinline__ SigPair sig_pair(float z) {
   const float e = expf(-fabsf(z));
-  const float r = 1.0f / (1.0f + e);
+  const float r = div_fast(1.f, 1.f + e);
   const float er = e * r;
   return z >= 0.f ? SigPair{r, er} : SigPair{er, r};
 }
@@ -117,15 +122,6 @@ __device__ __forceinline__ float div_fast(float a, float b) {
   const float r = __builtin_amdgcn_rcpf(b);
   const float q = a * r;
   return fmaf(fmaf(-b, q, a), r, q);
-}
-
-// sigma(z) for the sweep (and the h-side gradient's residual): accurate expf, 1/(1+e) by v_rcp and one
-// Newton step (div_fast)
-__device__ __forceinline__ SigPair sig_sweep2(float z) {   // sigma(z) and 1 - sigma(z) without cancellation
-  const float e = expf(-fabsf(z));
-  const float r = div_fast(1.f, 1.f + e);
-  const float er = e * r;
-  return z >= 0.f ? SigPair{r, er} : SigPair{er, r};
 }
 
 // phi(z) and phi'(z) of the h-side gradient's residual R = (phi(z) - tgt) phi'(z) (admm.py:302-312): the

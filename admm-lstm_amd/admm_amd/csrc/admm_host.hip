@@ -366,8 +366,7 @@ int stage_weights(AdmmCtx* c, int side, hipStream_t s) {
   if (c->trace_r[side]) {   // the residual this stage's G was formed from, as that kernel formed it
     if (!fast) HIP_TRY(hipMemcpyAsync(c->trace_r[side], c->R, (size_t)4 * g.BT() * g.H * sizeof(float),
                                       hipMemcpyDeviceToDevice, s));
-    else if (side == 0) launch_debug_resid(g, gsrc == c->gx_slab ? 0 : 1, c->zc, c->tgt, c->trace_r[0], s);
-    else launch_debug_resid(g, 1, zh, c->tgt, c->trace_r[1], s);
+    else launch_debug_resid(g, side == 0 ? c->zc : zh, c->tgt, c->trace_r[side], s);
   }
   // one process, split3 Q GEMM: the h side's reduce also forms the split G image for k_qgemm3 (no
   // k_split_g launch); several processes split it after the all-reduce

@@ -169,7 +169,7 @@ struct SweepRes {
 
 __device__ __forceinline__ SweepRes sweep_point(const Hyper& hp, const SweepIn& v, bool last) {
   const float ri = hp.rho[0], rf = hp.rho[1], rg = hp.rho[2], ro = hp.rho[3], rc = hp.rho[4], rh = hp.rho[5];
-  const SigPair pi = sig_sweep2(v.zi), pf = sig_sweep2(v.zf), po = sig_sweep2(v.zo);
+  const SigPair pi = sig_pair(v.zi), pf = sig_pair(v.zf), po = sig_pair(v.zo);
   const float ai = pi.s, af = pf.s, ag = tanhf(v.zg), ao = po.s;
   const float f0 = v.f0, g0 = v.g0, c0 = v.c0, h0 = v.h0, cp = v.cp;
   const float li = v.li, lf = v.lf, lg = v.lg, lo = v.lo, lc = v.lc, lh = v.lh;
@@ -3783,38 +3783,24 @@ void launch_trial_debug(int64_t n, int tanh_gate, int kbase, const float* z, con
 }
 
 // Test hook (admm_debug_trace_resid): the residual R_q = (phi(z) - tgt) phi'(z) of one weight
-// stage, element by element with the activation of the kernel that formed it there (the
+// stage, element by element with the activation every stage forms it with (sig_pair / tanhf: the
+// sweep's x-stage G_x partials, k_resid_gx, and the h stage's k_atr3w / k_atr_fused staging; the
 // admm.py:302-312 residual), so a test can recompute G = rho A^T R on identical operands.
-//   mode 0: the persistent sweep's (sweep_point: sig_sweep2 / tanhf; the x stage's G_x partials)
-//   mode 1: phi_acc (sig_pair / tanhf, the stored gates' activation): k_resid_gx's, and the h stage's
-//           k_atr3w / k_atr_fused staging
-template <int MODE>
 __global__ __launch_bounds__(kThreads) void k_debug_resid(int64_t n, const float* __restrict__ z,
                                                            const float* __restrict__ tgt, float* __restrict__ R) {
   for (int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x; i < 4 * n; i += (int64_t)gridDim.x * kThreads) {
-    const bool th = i / n == 2;
     const float zz = z[i], tt = tgt[i];
     float phi, dphi;
-    if (MODE == 1) {
-      if (th) phi_acc<true>(zz, phi, dphi);
-      else phi_acc<false>(zz, phi, dphi);
-    } else if (th) {
-      phi = tanhf(zz);
-      dphi = 1.f - phi * phi;
-    } else {
-      const SigPair sp = sig_sweep2(zz);
-      phi = sp.s;
-      dphi = sp.s * sp.sc;
-    }
+    if (i / n == 2) phi_acc<true>(zz, phi, dphi);
+    else phi_acc<false>(zz, phi, dphi);
     R[i] = (phi - tt) * dphi;
   }
 }
 
-void launch_debug_resid(const Geom& g, int mode, const float* z, const float* tgt, float* R, hipStream_t s) {
+void launch_debug_resid(const Geom& g, const float* z, const float* tgt, float* R, hipStream_t s) {
   const int64_t n = g.BT() * g.H;
   const int nb = (int)std::min<int64_t>((4 * n + kThreads - 1) / kThreads, 8192);
-  if (mode == 1) k_debug_resid<1><<<nb, kThreads, 0, s>>>(n, z, tgt, R);
-  else k_debug_resid<0><<<nb, kThreads, 0, s>>>(n, z, tgt, R);
+  k_debug_resid<<<nb, kThreads, 0, s>>>(n, z, tgt, R);
 }
 
 void launch_trial_reduce(const Geom& g, int pass, const double* part, int nblk, const int* found, double* sums,

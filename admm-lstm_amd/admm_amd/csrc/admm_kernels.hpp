@@ -202,9 +202,8 @@ void launch_trial(const Geom& g, int pass, const float* zc, const float* tgt, co
 // test hook: part[blk][J] for caller-provided z, tgt, q of one gate
 void launch_trial_debug(int64_t n, int tanh_gate, int kbase, const float* z, const float* tgt, const float* q,
                         double* part, int nblk, hipStream_t s);
-// test hook: R[4][BT][H] = (phi(z) - tgt) phi'(z) with the activation of the kernel that forms it
-// in the step (mode 0: the persistent sweep's, 1: k_resid_gx's, 2: phi_fast of the h stage)
-void launch_debug_resid(const Geom& g, int mode, const float* z, const float* tgt, float* R, hipStream_t s);
+// test hook: R[4][BT][H] = (phi(z) - tgt) phi'(z) with the activation every stage forms it with (phi_acc)
+void launch_debug_resid(const Geom& g, const float* z, const float* tgt, float* R, hipStream_t s);
 // sums[q][0..J) = sum_blk part[q][k] ; sums[q][J] = sum d0^2 (= 2 f(W)/rho)
 void launch_trial_reduce(const Geom& g, int pass, const double* part, int nblk, const int* found, double* sums,
                          hipStream_t s);

@@ -1,7 +1,7 @@
-// Exhaustive check (GPU box, one-off): is the sweep's sigmoid (sig_sweep2: expf, then 1/(1+e) by div_fast =
-// v_rcp + one Newton step) bit-identical to the stored gates' (sig_pair: expf, then the IEEE quotient) for
-// every finite float z?  Both pieces (sigma, 1 - sigma) are compared; also div_fast(1, d) against 1.f / d
-// for every float d in [1, 2] (the denominators 1 + e take).  Prints the mismatch counts.
+// Exhaustive check (GPU box, one-off): is the library's sigmoid (sig_pair: expf, then 1/(1+e) by div_fast =
+// v_rcp + one Newton step) bit-identical to the expf + IEEE-quotient form (sig_ieee below) for every finite
+// float z?  Both pieces (sigma, 1 - sigma) are compared; also div_fast(1, d) against 1.f / d for every
+// float d in [1, 2] (the denominators 1 + e take).  Prints the mismatch counts (profiles/r06f_sigcheck.txt).
 //   hipcc -O3 --offload-arch=gfx950 -I../include -Iadmm-lstm_amd/admm_amd/csrc tools/sigcheck.hip -o tools/sigcheck
 #include <hip/hip_runtime.h>
 #include <cstdio>
@@ -9,13 +9,20 @@
 
 using namespace admm;
 
+__device__ __forceinline__ SigPair sig_ieee(float z) {
+  const float e = expf(-fabsf(z));
+  const float r = 1.0f / (1.0f + e);
+  const float er = e * r;
+  return z >= 0.f ? SigPair{r, er} : SigPair{er, r};
+}
+
 __global__ void k_sig(unsigned long long* bad, unsigned long long* first) {
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
   unsigned long long nb = 0;
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < (1ull << 32); i += stride) {
     const float z = __uint_as_float((unsigned)i);
     if (!isfinite(z)) continue;
-    const SigPair a = sig_pair(z), b = sig_sweep2(z);
+    const SigPair a = sig_ieee(z), b = sig_pair(z);
     if (__float_as_uint(a.s) != __float_as_uint(b.s) || __float_as_uint(a.sc) != __float_as_uint(b.sc)) {
       ++nb;
       atomicMin(first, (unsigned long long)i);
@@ -44,7 +51,7 @@ int main() {
   if (hipDeviceSynchronize() != hipSuccess) return 2;
   unsigned long long h[3];
   (void)hipMemcpy(h, d, sizeof h, hipMemcpyDeviceToHost);
-  printf("sig_pair vs sig_sweep2 over all finite floats: %llu mismatches (first at bits 0x%llx)\n", h[0],
+  printf("sig_ieee vs sig_pair (div_fast) over all finite floats: %llu mismatches (first at bits 0x%llx)\n", h[0],
          h[0] ? h[1] : 0ull);
   printf("div_fast(1, d) vs 1.f / d over all floats d in [1, 2]: %llu mismatches\n", h[2]);
   return 0;

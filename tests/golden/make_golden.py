@@ -64,6 +64,8 @@ CASES = {
     # same capture on 4 threads (a different reduction order) as the reference's own noise floor
     'c3_25':        ('admm', False, 'uniform', 8192, 32, 16, 256, 25, False, 'GoogleStock'),
     'c3_25_t4':     ('admm', False, 'uniform', 8192, 32, 16, 256, 25, False, 'GoogleStock'),
+    # C5's per-GPU shape over 10 steps (the second BASELINE config's arithmetic over a longer horizon)
+    'c5_10':        ('no_dual_y', False, 'rw', 4096, 64, 1, 512, 10, False, 'GoogleStock'),
     # C4's global problem (65536 samples; the 8-GPU run shards exactly this) on one device
     'c4g':          ('admm', False, 'uniform', 65536, 32, 16, 256, 3, False, 'GoogleStock'),
     # perturbed starting state (golden_io.perturb_state: 1e-2 noise on gates and duals), so that the
@@ -82,6 +84,7 @@ CASES = {
 COMPACT = {'c3': {'full_w': (1, 2, 3, 4, 5), 'fp64': True},
            'c3_25': {'full_w': (5, 10, 15, 20, 25), 'fp64': False},
            'c3_25_t4': {'full_w': (25,), 'fp64': False},
+           'c5_10': {'full_w': (5, 10), 'fp64': False},
            'c5_1gpu': {'full_w': (3,), 'fp64': False},
            'c4g': {'full_w': (3,), 'fp64': False},
            't4_pert_h256': {'full_w': (1, 2, 3), 'fp64': True},
@@ -92,7 +95,7 @@ PERTURB = {'t4_pert_h256': {'seed': 11, 'scale': 1e-2}, 't4_pert_h512': {'seed':
            't32_pert_h256': {'seed': 11, 'scale': 1e-2}}
 WSTRIDE = 16
 # torch CPU threads per case (default: whatever torch picks, 8 in this container)
-THREADS = {'c3_25': 8, 'c3_25_t4': 4}
+THREADS = {'c3_25': 8, 'c3_25_t4': 4, 'c5_10': 8}
 
 
 def goog_windows():

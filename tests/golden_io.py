@@ -128,9 +128,9 @@ _NAMES = sorted(f[:-4] for f in os.listdir(GOLDEN) if f.endswith('.npz') and not
 # tests/test_gpu_weight_phase.py runs them
 PERTURBED = [n for n in _NAMES if Golden(n).meta.get('perturb')]
 COMPACT = [n for n in _NAMES if Golden(n).compact and n not in PERTURBED]
-# long full-size trajectories (the bench's own 25 steps of C3, captured at two thread counts):
-# tests/test_gpu_trajectory.py runs them
-LONG = [n for n in COMPACT if Golden(n).meta['steps'] >= 20]
+# long full-size trajectories (the bench's own 25 steps of C3, captured at two thread counts, and 10 steps
+# of C5's per-GPU shape): tests/test_gpu_trajectory.py runs them
+LONG = [n for n in COMPACT if Golden(n).meta['steps'] >= 10]
 # full-size fixtures the reference itself produced, and those the oracle produced (c5g)
 COMPACT_REF = [n for n in COMPACT if Golden(n).source == 'reference' and n not in LONG]
 COMPACT_ORACLE = [n for n in COMPACT if Golden(n).source == 'oracle' and n not in LONG]

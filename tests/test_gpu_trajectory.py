@@ -24,7 +24,10 @@ Two runs through the C ABI, per step:
   GPU-side fp32 oracle is, at every step (round 6: with the h-side gradient's residual on the stored
   gates' activation instead of phi_fast).
 
-Set ``ADMM_PARITY_OUT=<dir>`` for a JSON record per run (``parity_c3_25_{free,forced}.json``).
+``c5_10`` (round 6) is the same pair of runs at C5's per-GPU shape (no_dual_y, random-walk windows, B=4096,
+T=64, D=1, H=512) over 10 steps; it has no second capture, so its free run reports no thread-count spread.
+
+Set ``ADMM_PARITY_OUT=<dir>`` for a JSON record per run (``parity_<fixture>_{free,forced}.json``).
 """
 import ctypes
 import functools
@@ -74,10 +77,17 @@ def _compare(g, s, name, got):
     return _rel_wdiff(got, want)
 
 
-def ref_spread(s):
+# fixture -> its second capture on another thread count (the reference's own spread), or None
+FIXTURES = {'c3_25': 'c3_25_t4', 'c5_10': None}
+
+
+def ref_spread(name, s):
     """The reference's own 8- vs 4-thread spread at step s: loss (relative) and the largest weight
-    difference relative to the weight's largest entry (over the entries both captures keep)."""
-    g8, g4 = _golden('c3_25'), _golden('c3_25_t4')
+    difference relative to the weight's largest entry (over the entries both captures keep); (None, None)
+    without a second capture."""
+    if not FIXTURES[name]:
+        return None, None
+    g8, g4 = _golden(name), _golden(FIXTURES[name])
     loss = abs(g8.losses[s] - g4.losses[s]) / abs(g8.losses[s])
     w = 0.0
     for n in ('x2i', 'h2i', 'x2f', 'h2f', 'x2g', 'h2g', 'x2o', 'h2o', 'out'):
@@ -97,12 +107,12 @@ def _keep(g, s, name, w):
     return w
 
 
-def _oracle_forced(dtype, dev):
+def _oracle_forced(name, dtype, dev):
     """The oracle (the reference's op structure) on the GPU's torch ops in dtype, replaying the reference's
     decisions (Stepper.force): the exact trajectory (fp64) and another fp32 platform (fp32).  Returns the
     weights after each step as CPU fp64 tensors."""
     from oracle import admm_oracle as O
-    g = _golden('c3_25')
+    g = _golden(name)
     torch.manual_seed(0)
     W = {k: v.to(dev, dtype) for k, v in O.init_weights(g.D, g.H, g.O).items()}
     st = O.init_state(g.x.to(dev, dtype), g.y.to(dev, dtype), W)
@@ -117,9 +127,9 @@ def _oracle_forced(dtype, dev):
     return out
 
 
-def _trajectory(mods, dev, force: bool, keep_weights: bool = False):
+def _trajectory(name, mods, dev, force: bool, keep_weights: bool = False):
     from admm_amd import _native as N
-    g = _golden('c3_25')
+    g = _golden(name)
     model, opt = _optimizer(g, mods, dev)
     x, y = g.x.to(dev), g.y.to(dev)
     lib = opt._lib
@@ -143,8 +153,9 @@ def _trajectory(mods, dev, force: bool, keep_weights: bool = False):
             assert ks == ref_k, (s, ks, ref_k)
         loss = _loss(model, x, y)
         wd = {n: _compare(g, s, n, p.detach().cpu()) for n, p in model.named_parameters()}
-        sl, sw = ref_spread(s)
-        recs.append({'step': s, 'loss': loss, 'ref_loss': g.losses[s], 'ref4_loss': _golden('c3_25_t4').losses[s],
+        sl, sw = ref_spread(name, s)
+        recs.append({'step': s, 'loss': loss, 'ref_loss': g.losses[s],
+                     'ref4_loss': _golden(FIXTURES[name]).losses[s] if FIXTURES[name] else None,
                      'loss_rel': abs(loss - g.losses[s]) / abs(g.losses[s]), 'ref_spread_loss': sl,
                      'wdiff_max': max(wd.values()), 'wdiff': wd, 'ref_spread_w': sw,
                      'k': ks, 'ref_k': ref_k, 'own_k': own, 'theta_h': st['theta_h']})
@@ -155,33 +166,35 @@ def _trajectory(mods, dev, force: bool, keep_weights: bool = False):
     del opt, model
     torch.cuda.empty_cache()
     if not force:
-        _write('free', recs)
+        _write(name, 'free', recs)
     return recs
 
 
-def _write(run, recs):
+def _write(name, run, recs):
     out = os.environ.get('ADMM_PARITY_OUT')
     if out:
         os.makedirs(out, exist_ok=True)
-        with open(os.path.join(out, f'parity_c3_25_{run}.json'), 'w') as f:
+        with open(os.path.join(out, f'parity_{name}_{run}.json'), 'w') as f:
             json.dump({'steps': [{k: v for k, v in r.items() if k != 'W'} for r in recs]}, f, indent=1)
 
 
-def test_bench_trajectory_free_run(mods, dev):
+@pytest.mark.parametrize('name', sorted(FIXTURES))
+def test_bench_trajectory_free_run(name, mods, dev):
     """The bench's trajectory with the library's own decisions: loss within 1e-5 of the reference at
     every step 1..25 (the bench's final_train_mse is step 25's)."""
-    recs = _trajectory(mods, dev, force=False)
+    recs = _trajectory(name, mods, dev, force=False)
     for r in recs:
         assert r['loss_rel'] <= LOSS_RTOL, (r['step'], r['loss'], r['ref_loss'], [q['loss_rel'] for q in recs])
 
 
-def test_bench_trajectory_forced_decisions(mods, dev):
-    """The same 25 steps replaying the reference's decisions: the loss within 1e-5 at every step, and the
+@pytest.mark.parametrize('name', sorted(FIXTURES))
+def test_bench_trajectory_forced_decisions(name, mods, dev):
+    """The same steps replaying the reference's decisions: the loss within 1e-5 at every step, and the
     library's weights at most DRIFT_VS_REF x as far from the exact (fp64) trajectory as the reference's."""
-    recs = _trajectory(mods, dev, force=True, keep_weights=True)
-    w64 = _oracle_forced(torch.float64, dev)
-    w32 = _oracle_forced(torch.float32, dev)
-    g = _golden('c3_25')
+    recs = _trajectory(name, mods, dev, force=True, keep_weights=True)
+    w64 = _oracle_forced(name, torch.float64, dev)
+    w32 = _oracle_forced(name, torch.float32, dev)
+    g = _golden(name)
     for r, e64, e32 in zip(recs, w64, w32):
         s = r['step']
         lib64 = ref64 = gpu32ref = 0.0
@@ -191,7 +204,7 @@ def test_bench_trajectory_forced_decisions(mods, dev):
             ref64 = max(ref64, _rel_wdiff(ref, _keep(g, s, n, e64[n])))
             gpu32ref = max(gpu32ref, _rel_wdiff(_keep(g, s, n, e32[n]), ref))
         r.update({'lib_vs_fp64': lib64, 'ref_vs_fp64': ref64, 'gpu32_oracle_vs_ref': gpu32ref})
-    _write('forced', recs)
+    _write(name, 'forced', recs)
     for r in recs:
         assert r['loss_rel'] <= LOSS_RTOL, (r['step'], r['loss'], r['ref_loss'])
         table = [(q['step'], q['lib_vs_fp64'], q['ref_vs_fp64'], q['wdiff_max'], q['gpu32_oracle_vs_ref']) for q in recs]

@@ -118,7 +118,7 @@ def test_fixture_sources():
     case (test_gpu_fullsize.test_fullsize_matches_oracle_fixture)."""
     assert COMPACT_ORACLE == ['c5g']
     assert set(COMPACT_REF) == {'c3', 'c5_1gpu', 'c4g'}
-    assert set(LONG) == {'c3_25', 'c3_25_t4'}
+    assert set(LONG) == {'c3_25', 'c3_25_t4', 'c5_10'}
     for n in ALL + PERTURBED + COMPACT_REF + LONG:
         g = Golden(n)
         assert g.source == 'reference', n

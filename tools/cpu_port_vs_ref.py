@@ -27,7 +27,7 @@ def child(impl, cfg, threads, steps):
     import bench
     B, T, D, H, variant, gen = bench.CONFIGS[cfg]
     x, y = bench.make_data(gen, B, T, D)
-    times, losses = [], []
+    times, losses, cpu = [], [], []
     if impl == 'ref':
         os.chdir('/tmp')   # the reference's logger writes logs/ in the cwd
         # bench put this repo's drop-in package on the path: the reference's own modules instead
@@ -44,9 +44,10 @@ def child(impl, cfg, threads, steps):
         model = LSTM(D, H, 1)
         opt = admm.ADMMBasedOptimizer(model, (x, y), example_parameter_dictionary['GoogleStock'], verbose=False)
         for _ in range(steps):
-            t0 = time.time()
+            t0, c0 = time.time(), time.process_time()
             opt.step()
             times.append(time.time() - t0)
+            cpu.append(time.process_time() - c0)
             losses.append(float(torch.nn.functional.mse_loss(model(x), y)))
     else:
         sys.path.insert(0, os.path.join(ROOT, 'admm-lstm_amd'))
@@ -57,11 +58,12 @@ def child(impl, cfg, threads, steps):
         st = O.init_state(x, y, W)
         stp = O.Stepper(O.Hyper.from_dict(example_parameter_dictionary['GoogleStock'], variant))
         for _ in range(steps):
-            t0 = time.time()
+            t0, c0 = time.time(), time.process_time()
             stp.step(st)
             times.append(time.time() - t0)
+            cpu.append(time.process_time() - c0)
             losses.append(O.mse(x, y, st.W))
-    print(json.dumps({'impl': impl, 'config': cfg, 'threads': threads, 'step_s': times, 'loss': losses}))
+    print(json.dumps({'impl': impl, 'config': cfg, 'threads': threads, 'step_s': times, 'cpu_s': cpu, 'loss': losses}))
 
 
 def main():
@@ -85,9 +87,12 @@ def main():
                 rec = json.loads(out.stdout.strip().splitlines()[-1])
                 st = sorted(rec['step_s'][1:])
                 rec['median_2_on'] = st[len(st) // 2]
+                sc = sorted(rec['cpu_s'][1:])
+                rec['cpu_median_2_on'] = sc[len(sc) // 2]
                 rec['round'] = r
                 runs.append(rec)
                 print(f"{cfg} round {r} {impl}: median of steps 2-{a.steps} {rec['median_2_on']:.3f} s "
+                      f"(process CPU {rec['cpu_median_2_on']:.2f} s) "
                       f"(steps {', '.join(f'{t:.2f}' for t in rec['step_s'])})", flush=True)
     summary = {}
     for cfg in a.configs.split(','):
@@ -95,7 +100,16 @@ def main():
                for impl in ('port', 'ref')}
         lp = [r['loss'] for r in runs if r['config'] == cfg and r['impl'] == 'port'][0]
         lr = [r['loss'] for r in runs if r['config'] == cfg and r['impl'] == 'ref'][0]
-        summary[cfg] = {'port_s': med['port'], 'ref_s': med['ref'],
+        cmed = {impl: sorted(r['cpu_median_2_on'] for r in runs if r['config'] == cfg and r['impl'] == impl)
+                for impl in ('port', 'ref')}
+        rounds = sorted(set(r['round'] for r in runs if r['config'] == cfg))
+        per_round = [[r['median_2_on'] for r in runs if r['config'] == cfg and r['round'] == k and r['impl'] == 'port'][0]
+                     / [r['median_2_on'] for r in runs if r['config'] == cfg and r['round'] == k and r['impl'] == 'ref'][0]
+                     for k in rounds]
+        summary[cfg] = {'port_cpu_s': cmed['port'], 'ref_cpu_s': cmed['ref'],
+                        'port_over_ref_cpu': sum(cmed['port']) / sum(cmed['ref']),
+                        'port_over_ref_per_round': per_round,
+                        'port_s': med['port'], 'ref_s': med['ref'],
                         'port_over_ref': sum(med['port']) / sum(med['ref']),
                         'max_rel_loss_diff': max(abs(p - q) / abs(q) for p, q in zip(lp, lr))}
     doc = {'note': 'tools/cpu_port_vs_ref.py in the build container (no GPU): the CPU port against the reference '

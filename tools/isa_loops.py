@@ -102,9 +102,11 @@ def main():
     ap.add_argument('--kernel', default=r'k_sweep_rowsILi8ELi1ELb1ELi32ELi1E')
     ap.add_argument('--min-stores', type=int, default=15)
     ap.add_argument('--min-loads', type=int, default=10)
+    ap.add_argument('--ops', type=int, default=0, help='also print the N most frequent mnemonics of the largest loop')
+    ap.add_argument('--asm', help='read this assembly file instead of compiling')
     ap.add_argument('src', nargs='?', default='admm_kernels.hip')
     a = ap.parse_args()
-    lines = compile_asm(a.src)
+    lines = open(a.asm).read().splitlines() if a.asm else compile_asm(a.src)
     rx = re.compile(a.kernel)
     found = False
     for name, body in functions(lines):
@@ -126,6 +128,11 @@ def main():
             print(f'  loop {lp[0][3][:40]!r} .. {lp[-1][3][:40]!r}: {len(lp)} instructions')
             for k, v in census(lp).items():
                 print(f'    {k:45s} {v:5d}')
+        if a.ops:
+            ops = collections.Counter(x[2] for x in max(cand, key=len))
+            print('  most frequent mnemonics of the largest loop:')
+            for mn, c in ops.most_common(a.ops):
+                print(f'    {mn:45s} {c:5d}')
     if not found:
         sys.exit(f'no kernel matches {a.kernel}')
 

@@ -348,6 +348,34 @@ def cgroup_cpus():
     return None if a == 'max' else round(int(a) / int(b), 2)
 
 
+def port_vs_reference(cfg_name: str):
+    """The CPU port's time against the reference's own, from the build container's alternated records
+    (tools/cpu_port_vs_ref.py -> profiles/r06_cpu_port_vs_ref_*.json; the reference never travels to the
+    GPU box, so the ratio is measured there and reported here beside the port's time): port / reference
+    per record of this config (pooled medians, wall and, where recorded, process CPU time), with the
+    per-round ratios.  Below 1 the port is faster than the reference, i.e. the GPU/CPU ratio is understated."""
+    import glob
+    out = []
+    for f in sorted(glob.glob(os.path.join(ROOT, 'profiles', 'r06_cpu_port_vs_ref_*.json'))):
+        try:
+            with open(f) as fh:
+                d = json.load(fh)
+        except (OSError, ValueError):
+            continue
+        sm = d.get('summary', {}).get(cfg_name)
+        if not sm or 'port_over_ref' not in sm:
+            continue
+        r = {'source': os.path.relpath(f, ROOT), 'threads': d.get('host', {}).get('threads'),
+             'rounds': len(sm.get('port_s', [])), 'port_over_ref_wall': round(sm['port_over_ref'], 3)}
+        if 'port_over_ref_cpu' in sm:
+            r['port_over_ref_cpu_time'] = round(sm['port_over_ref_cpu'], 3)
+        if 'port_over_ref_per_round' in sm:
+            r['per_round_cpu_time'] = [round(v, 3) for v in sm['port_over_ref_per_round']]
+        r['max_rel_loss_diff'] = sm.get('max_rel_loss_diff')
+        out.append(r)
+    return out or None
+
+
 def cpu_baseline(cfg_name: str, timed_steps: int = 5, crosscheck_threads: int = 8):
     """SURVEY.md 8(d) CPU-baseline protocol on this host: the CPU oracle (a port of the reference's
     op structure, oracle/admm_oracle.py) on the FULL batch of the config, on all physical cores of the
@@ -415,6 +443,7 @@ def cpu_baseline(cfg_name: str, timed_steps: int = 5, crosscheck_threads: int = 
         'crosscheck': {'threads': crosscheck_threads, 'step_s': round(cross, 3)} if cross else None,
         'host_cpu': {'model': model, 'sockets': sockets, 'physical_cores_per_socket': per_socket,
                      'socket': socket, 'pinned_cpus': cores, 'cgroup_cpu_quota': quota},
+        'port_vs_reference': port_vs_reference(cfg_name),
     }
 
 

@@ -370,7 +370,9 @@ def port_vs_reference(cfg_name: str):
         if 'port_over_ref_cpu' in sm:
             r['port_over_ref_cpu_time'] = round(sm['port_over_ref_cpu'], 3)
         if 'port_over_ref_per_round' in sm:
+            pr = sorted(sm['port_over_ref_per_round'])
             r['per_round_cpu_time'] = [round(v, 3) for v in sm['port_over_ref_per_round']]
+            r['per_round_median'] = round(pr[len(pr) // 2], 3)   # robust to one disturbed round
         r['max_rel_loss_diff'] = sm.get('max_rel_loss_diff')
         out.append(r)
     return out or None

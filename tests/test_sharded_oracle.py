@@ -8,6 +8,7 @@ rows must reproduce the 1-rank full-batch run -- the same decomposition the HIP 
 implements with RCCL all-reduces (admm_host.hip).
 """
 import os
+import socket
 
 import pytest
 import torch
@@ -80,7 +81,9 @@ def test_two_gloo_ranks_equal_one(variant):
         stp.step(st)
     ctx = mp.get_context('spawn')
     q = ctx.Queue()
-    port = 29500 + (os.getpid() % 1000)
+    with socket.socket() as sk:   # a free port (parallel test workers must not collide)
+        sk.bind(('127.0.0.1', 0))
+        port = sk.getsockname()[1]
     procs = [ctx.Process(target=_worker, args=(r, 2, port, variant, steps, q)) for r in range(2)]
     for p in procs:
         p.start()

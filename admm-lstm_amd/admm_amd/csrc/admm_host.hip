@@ -138,6 +138,7 @@ struct AdmmCtx {
   // range [8] (device): SweepT::range's maxima from the last persistent sweep ([0..4], valid when
   // range_valid) and max_row sum_d |x_d| ([5], valid when x1_valid)
   bool atr_f16 = true;
+  bool atr_wide = true;    // ... and at H = 512 in 512 x 128 tiles (ADMM_ATR_WIDE=0: 256 x 256)
   float* range = nullptr;
   bool range_valid = false, x1_valid = false;
   // column-split sweep (strong-scaling ranks, sweep_rows_nc > 1): the h_t hand-off granules
@@ -339,7 +340,7 @@ int stage_weights(AdmmCtx* c, int side, hipStream_t s) {
     }
     ProfScope ps(c, ADMM_PROF_ATR_H, s);
     launch_atr3(g, c->buf.gates[ADMM_H], zh, c->tgt, c->gslab, ns, s, f16 ? c->range : nullptr,
-                f16 ? c->dW : nullptr);
+                f16 ? c->dW : nullptr, c->atr_wide);
   } else if (fast) {
     ns = atr_splits(g, 1);
     ProfScope ps(c, ADMM_PROF_ATR_H, s);
@@ -601,6 +602,7 @@ int admm_create(const AdmmDims* dims, const AdmmParams* params, int device, Admm
   if (const char* e = std::getenv("ADMM_SPLIT3")) c->split3 = c->split3 && std::atoi(e) != 0;
   if (const char* e = std::getenv("ADMM_P16")) c->p16 = std::atoi(e) != 0;
   if (const char* e = std::getenv("ADMM_ATR_F16")) c->atr_f16 = std::atoi(e) != 0;
+  if (const char* e = std::getenv("ADMM_ATR_WIDE")) c->atr_wide = std::atoi(e) != 0;
   if (const char* e = std::getenv("ADMM_GRAPH")) c->graph = std::atoi(e) != 0;
   Hyper& h = c->hp;
   for (int i = 0; i < 7; ++i) h.rho[i] = params->rho[i];

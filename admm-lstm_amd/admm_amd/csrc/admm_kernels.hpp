@@ -261,9 +261,10 @@ size_t split3_gimg_floats(const Geom& g);
 int atr3_splits(const Geom& g);
 // range, dW non-null: k_atr3w on scaled-fp16 two-way splits, with the operand ranges the persistent
 // sweep left (SweepT::range, plus [5] = max_row sum_d |x_d|) and the x stage's decided update dW
-// [4][D][H]; else on split3 (both f32-accurate)
+// [4][D][H]; else on split3 (both f32-accurate).  wide_ok: the fp16 path at H = 512 takes 512 x 128
+// tiles instead of 256 x 256 (bit-identical slabs)
 void launch_atr3(const Geom& g, const float* Sh, const float* zc, const float* tgt, float* slab, int nsplit,
-                 hipStream_t s, const float* range = nullptr, const float* dW = nullptr);
+                 hipStream_t s, const float* range = nullptr, const float* dW = nullptr, bool wide_ok = true);
 // range[5] = max over rows of sum_d |x[row][d]| (atomicMax into a zeroed slot)
 void launch_x_l1max(const Geom& g, const float* x, float* range, hipStream_t s);
 // Q = Hprev G, the h-side trial direction: Hprev in two bf16 pieces, G rounded to bf16 (it enters

@@ -249,7 +249,8 @@ __device__ __forceinline__ int a3_off(int row, int col) {   // bf16 offset of (r
   return sub * A3_SUB + row * 128 + 8 * (ch ^ (((row & 3) << 2) | ((row >> 2) & 3))) + (cw & 4);
 }
 
-// k_atr3w: 8 waves as 2 (m) x 4 (j) of 128 x 64: 128 accumulators per lane, so two waves share each
+// k_atr3w: 8 waves as 2 (m) x 4 (j) of 128 x 64 (4 x 2 in the 512 x 128 tile of H = 512): 128
+// accumulators per lane, so two waves share each
 // SIMD and one wave's staging VALU (phi, phi', the split of R and Hprev) and waits issue while the
 // other's MFMAs run (at one wave per SIMD with 256 accumulators -- round 2's k_atr3 -- the staging
 // and the MFMAs of a wave serialised: 0.85 against 0.80 ms at C3).  Each wave stages two rows of
@@ -260,9 +261,20 @@ constexpr int A3W_THREADS = 512;
 #ifndef A3W_ABL
 #define A3W_ABL 0   // timing ablations for tools/build_lib_variant.sh: 1 no loads, 2 no MFMAs
 #endif
-struct Atr3wRing { float4 a[2], z[2], t[2]; };
+// One step's operand loads of a wave: BM = 256, two rows of 256 H_prev and 256 z / tgt columns
+// (one 1-KB row per wave-instruction); BM = 512, two rows of all 512 H_prev columns (four
+// instructions) and two rows of 128 z / tgt columns (one instruction: a half-wave per row).
+template <int BM>
+struct Atr3wRing {
+  static constexpr int NA = BM / 128, NZ = BM == 512 ? 1 : 2;
+  float4 a[NA], z[NZ], t[NZ];
+};
 
-// (mb, nb): the 256 x 256 block of G_q (H_prev columns 256 mb.., R columns 256 nb..).
+// Tile shapes (BM x BN, 128 accumulators per lane either way):
+//  BM = 256: (mb, nb) is the 256 x 256 block of G_q (H_prev columns 256 mb.., R columns 256 nb..);
+//  BM = 512 (H = 512): mb = 0, the 512 x 128 block of all H_prev columns and R columns 128 nb.., so
+//  that every R element is formed (phi, phi', the fp16 split) by one workgroup instead of two, and
+//  z / tgt are read once from HBM.  The per-output product sequence is the same: G is bit-identical.
 // NP = 3: split3 operands, six products (f32-accurate); the first h stage after the state is bound
 // or invalidated (no sweep has bounded the operands yet).
 // NP = 2, F16: two fp16 pieces instead (bf16 two-way splits, ~2^-16 per product, measured 1.3-3.7x
@@ -320,13 +332,24 @@ __device__ __forceinline__ float2 atr_scales(const Geom& g, int q, const float* 
   return make_float2(scale(hb), scale(rb));
 }
 
-template <bool TANH, int NP, bool F16 = false>
+template <int BM>
+struct A3T {
+  static constexpr int BN = BM == 512 ? 128 : 256;
+  static constexpr int PA = (BM / 128) * A3_SUB;   // one split piece of the Hprev operand
+  static constexpr int PR = (BN / 128) * A3_SUB;   // one split piece of the R operand
+  static constexpr int WM = BM / 128;              // waves along m (128 rows each); 8 / WM along j
+};
+
+template <bool TANH, int NP, bool F16 = false, int BM = 256>
 __device__ __forceinline__ void atr3w_body(const Geom& g, int q, int sp, int nsplit, int mb, int nb,
                                            const float* __restrict__ Sh, const float* __restrict__ zq,
                                            const float* __restrict__ tq, float* __restrict__ slab, __bf16* img,
                                            float2 scl = make_float2(1.f, 1.f)) {
   static_assert(!F16 || NP == 2, "fp16 operands come in two pieces");
-  using P = A3<256>;
+  static_assert(BM == 256 || BM == 512, "tile rows");
+  using P = A3T<BM>;
+  using Ring = Atr3wRing<BM>;
+  constexpr bool WIDE = BM == 512;
   const int H = g.H;
   const int64_t BT = g.BT();
   const int64_t per = ((BT + nsplit - 1) / nsplit + A3_KS - 1) / A3_KS * A3_KS;
@@ -340,21 +363,40 @@ __device__ __forceinline__ void atr3w_body(const Geom& g, int q, int sp, int nsp
   const __amdgpu_buffer_rsrc_t rT = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(tq), 0, (int)(BT * H * 4), kBufWord3);
   const int vo = 16 * lane;   // float4 column 4 lane of a 256-float row
   const int va = vo + 1024 * mb, vz = vo + 1024 * nb;   // + the block's first column
-  auto gload = [&](Atr3wRing& R, int64_t k0) {   // rows past r1 clamped; they meet R = 0 in put()
+  // WIDE: z / tgt rows 2 rg (lanes 0-31) and 2 rg + 1 (lanes 32-63), 128 columns from 128 nb
+  const int vzw = 16 * (lane & 31) + 512 * nb;
+  auto gload = [&](Ring& R, int64_t k0) {   // rows past r1 clamped; they meet R = 0 in put()
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const int64_t r = k0 + 2 * rg + i, row = r < r1 ? r : r1 - 1;
       if (A3W_ABL & 1) {   // timing ablation (tools only): no operand loads
-        R.a[i] = make_float4((float)row, 0.5f, 0.25f, 0.125f); R.z[i] = R.a[i]; R.t[i] = R.a[i];
+        const float4 f = make_float4((float)row, 0.5f, 0.25f, 0.125f);
+#pragma unroll
+        for (int h = 0; h < Ring::NA / 2; ++h) R.a[i * Ring::NA / 2 + h] = f;
+        if (i < Ring::NZ) { R.z[i] = f; R.t[i] = f; }
         continue;
       }
-      R.a[i] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rA, va, (int)(g.hrow(row) * H * 4), 0));
-      R.z[i] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rZ, vz, (int)(row * H * 4), 2));
-      R.t[i] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rT, vz, (int)(row * H * 4), 2));
+      if constexpr (WIDE) {
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+          R.a[2 * i + h] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rA, vo + 1024 * h,
+                                                                                            (int)(g.hrow(row) * H * 4), 0));
+      } else {
+        R.a[i] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rA, va, (int)(g.hrow(row) * H * 4), 0));
+        R.z[i] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rZ, vz, (int)(row * H * 4), 2));
+        R.t[i] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rT, vz, (int)(row * H * 4), 2));
+      }
+    }
+    if constexpr (WIDE) {
+      if (A3W_ABL & 1) return;
+      const int64_t r = k0 + 2 * rg, row = r < r1 ? r : r1 - 1;   // the first row (uniform)
+      const int vzr = vzw + ((lane >> 5) && r + 1 < r1 ? H * 4 : 0);   // the second: a row further
+      R.z[0] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rZ, vzr, (int)(row * H * 4), 2));
+      R.t[0] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rT, vzr, (int)(row * H * 4), 2));
     }
   };
   constexpr int STAGE = NP * (P::PA + P::PR);
-  auto put = [&](int st, const Atr3wRing& R, int64_t k0) {
+  auto put = [&](int st, const Ring& R, int64_t k0) {
     __bf16* A = img + st * STAGE;
     __bf16* B = A + NP * P::PA;
     bf16x4 p0, p1, p2;
@@ -362,18 +404,16 @@ __device__ __forceinline__ void atr3w_body(const Geom& g, int q, int sp, int nsp
       if constexpr (F16) split2h(v, p0, p1);
       else split3(v, p0, p1, p2);
     };
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int rr = 2 * rg + i;
-      const int o = a3_off(rr, 4 * lane);
-      if constexpr (F16) pieces(f32x4{R.a[i].x, R.a[i].y, R.a[i].z, R.a[i].w} * scl.x);
-      else pieces(f32x4{R.a[i].x, R.a[i].y, R.a[i].z, R.a[i].w});
+    auto put_a = [&](int o, const float4& a) {
+      if constexpr (F16) pieces(f32x4{a.x, a.y, a.z, a.w} * scl.x);
+      else pieces(f32x4{a.x, a.y, a.z, a.w});
       *reinterpret_cast<bf16x4*>(A + o) = p0;
       *reinterpret_cast<bf16x4*>(A + P::PA + o) = p1;
       if constexpr (NP == 3) *reinterpret_cast<bf16x4*>(A + 2 * P::PA + o) = p2;
-      const bool ok = k0 + rr < r1;
-      const float zz[4] = {R.z[i].x, R.z[i].y, R.z[i].z, R.z[i].w};
-      const float tt[4] = {R.t[i].x, R.t[i].y, R.t[i].z, R.t[i].w};
+    };
+    auto put_r = [&](int o, bool ok, const float4& z, const float4& t) {
+      const float zz[4] = {z.x, z.y, z.z, z.w};
+      const float tt[4] = {t.x, t.y, t.z, t.w};
       f32x4 rv;
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
@@ -386,6 +426,22 @@ __device__ __forceinline__ void atr3w_body(const Geom& g, int q, int sp, int nsp
       *reinterpret_cast<bf16x4*>(B + o) = p0;
       *reinterpret_cast<bf16x4*>(B + P::PR + o) = p1;
       if constexpr (NP == 3) *reinterpret_cast<bf16x4*>(B + 2 * P::PR + o) = p2;
+    };
+    if constexpr (WIDE) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int h = 0; h < 2; ++h) put_a(a3_off(2 * rg + i, 256 * h + 4 * lane), R.a[2 * i + h]);
+      const int rr = 2 * rg + (lane >> 5);
+      put_r(a3_off(rr, 4 * (lane & 31)), k0 + rr < r1, R.z[0], R.t[0]);
+    } else {
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int rr = 2 * rg + i;
+        const int o = a3_off(rr, 4 * lane);
+        put_a(o, R.a[i]);
+        put_r(o, k0 + rr < r1, R.z[i], R.t[i]);
+      }
     }
   };
   // transposed fragment reads: lane group gi = lane >> 4 takes columns +16 (gi & 1) and rows
@@ -402,7 +458,7 @@ __device__ __forceinline__ void atr3w_body(const Geom& g, int q, int sp, int nsp
       f[p] = bf16x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
     }
   };
-  const int wr = wave & 1, wc = wave >> 1;   // m half, 64-column quarter
+  const int wr = wave % P::WM, wc = wave / P::WM;   // 128-row m block, 64-column j block
   f32x16 acc[4][2];
   zero_acc(acc);
   auto compute = [&](int st) {
@@ -427,7 +483,7 @@ __device__ __forceinline__ void atr3w_body(const Geom& g, int q, int sp, int nsp
   // VALU into the MFMA stream (1 MFMA : 3-5 VALU : 1 DS), and the upper four waves staging before
   // multiplying (opposite phase to their SIMD partner: 0.84 against 0.76 ms, no spills in the loop).
   if (r0 < r1) {
-    Atr3wRing R0, R1;
+    Ring R0, R1;
     gload(R0, r0);
     gload(R1, r0 + ks);
     put(0, R0, r0);
@@ -443,7 +499,7 @@ __device__ __forceinline__ void atr3w_body(const Geom& g, int q, int sp, int nsp
       __syncthreads();
     }
   }
-  float* out = slab + ((int64_t)sp * 4 + q) * H * H + (int64_t)(256 * mb) * H + 256 * nb + wc * 64 + (lane & 31);
+  float* out = slab + ((int64_t)sp * 4 + q) * H * H + (int64_t)(BM * mb) * H + P::BN * nb + wc * 64 + (lane & 31);
   const float inv = F16 ? 1.f / (scl.x * scl.y) : 1.f;   // a power of two: exact
 #pragma unroll
   for (int mi = 0; mi < 4; ++mi)
@@ -455,21 +511,24 @@ __device__ __forceinline__ void atr3w_body(const Geom& g, int q, int sp, int nsp
     }
 }
 
-template <int NP, bool F16 = false>
+template <int NP, bool F16 = false, int BM = 256>
 __global__ __launch_bounds__(A3W_THREADS, 1) void k_atr3w(Geom g, const float* __restrict__ Sh,
                                                          const float* __restrict__ zc, const float* __restrict__ tgt,
                                                          float* __restrict__ slab, int nsplit,
                                                          const float* __restrict__ range, const float* __restrict__ dW) {
-  __shared__ __attribute__((aligned(16))) __bf16 img[2 * NP * (A3<256>::PA + A3<256>::PR)];
+  using P = A3T<BM>;
+  __shared__ __attribute__((aligned(16))) __bf16 img[2 * NP * (P::PA + P::PR)];
   int lid = xcd_swizzle(blockIdx.x, gridDim.x);
   const int q = lid % 4;          // the 4 gates of one split share the Hprev rows: same XCD
   lid /= 4;
-  const int nt = g.H / 256, tl = lid % (nt * nt), sp = lid / (nt * nt);
+  const int nmb = g.H / BM, nnb = g.H / P::BN, tl = lid % (nmb * nnb), sp = lid / (nmb * nnb);
   const int64_t n = g.BT() * g.H;
   float2 scl = make_float2(1.f, 1.f);
   if constexpr (F16) scl = atr_scales(g, q, range, dW, reinterpret_cast<float*>(img));
-  if (q == 2) atr3w_body<true, NP, F16>(g, q, sp, nsplit, tl / nt, tl % nt, Sh, zc + q * n, tgt + q * n, slab, img, scl);
-  else atr3w_body<false, NP, F16>(g, q, sp, nsplit, tl / nt, tl % nt, Sh, zc + q * n, tgt + q * n, slab, img, scl);
+  if (q == 2)
+    atr3w_body<true, NP, F16, BM>(g, q, sp, nsplit, tl / nnb, tl % nnb, Sh, zc + q * n, tgt + q * n, slab, img, scl);
+  else
+    atr3w_body<false, NP, F16, BM>(g, q, sp, nsplit, tl / nnb, tl % nnb, Sh, zc + q * n, tgt + q * n, slab, img, scl);
 }
 
 }  // namespace
@@ -507,13 +566,17 @@ int atr3_splits(const Geom& g) {
 }
 
 void launch_atr3(const Geom& g, const float* Sh, const float* zc, const float* tgt, float* slab, int nsplit,
-                 hipStream_t s, const float* range, const float* dW) {
-  // 256 x 256 blocks of each gate's G (H % 256 == 0, split3_ok), nsplit row ranges
+                 hipStream_t s, const float* range, const float* dW, bool wide_ok) {
+  // 256 x 256 blocks of each gate's G (H % 256 == 0, split3_ok), nsplit row ranges; at H = 512 the
+  // fp16 path takes 512 x 128 blocks instead (the same count, every R element staged once)
   const int nt = g.H / 256, nb = 4 * nt * nt * nsplit;
-  if (range && dW)   // scaled fp16 two-way splits: f32-accurate at two pieces' matrix work
-    k_atr3w<2, true><<<nb, A3W_THREADS, 0, s>>>(g, Sh, zc, tgt, slab, nsplit, range, dW);
-  else
+  const bool wide = wide_ok && g.H == 512;
+  if (range && dW) {   // scaled fp16 two-way splits: f32-accurate at two pieces' matrix work
+    if (wide) k_atr3w<2, true, 512><<<nb, A3W_THREADS, 0, s>>>(g, Sh, zc, tgt, slab, nsplit, range, dW);
+    else k_atr3w<2, true><<<nb, A3W_THREADS, 0, s>>>(g, Sh, zc, tgt, slab, nsplit, range, dW);
+  } else {   // (once per bound state; the 512 x 128 tile spills here with three pieces)
     k_atr3w<3><<<nb, A3W_THREADS, 0, s>>>(g, Sh, zc, tgt, slab, nsplit, nullptr, nullptr);
+  }
 }
 
 void launch_split_g(const Geom& g, const float* G, float* gimg, hipStream_t s) {

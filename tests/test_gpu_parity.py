@@ -759,6 +759,37 @@ def test_tgt_from_sweep_bit_identical(shape, mods, dev, monkeypatch):
     assert torch.equal(out[0][1], out[1][1])
 
 
+@pytest.mark.parametrize('shape', [(130, 3, 1, 512), (300, 4, 2, 512)])
+def test_atr_wide_tile_bit_identical(shape, mods, dev, monkeypatch):
+    """At H = 512 the h-side gradient's fp16 path (k_atr3w<2, true>, every step after the first)
+    stages 512 x 128 tiles, so that each R element is formed once (default), instead of 256 x 256
+    (ADMM_ATR_WIDE=0).  Each output's product sequence is the same, so the slabs, and with them the
+    whole trajectory, must be bit-identical.  B T = 900 and 1200 cover a ragged last 16-row step
+    (the two-row z / tgt load of a half-wave each, clamped rows)."""
+    from blocks.lstm import LSTM
+    from parameters import example_parameter_dictionary
+    admm, _ = mods
+    admm.with_dual_y = False
+    B, T, D, H = shape
+    g = torch.Generator().manual_seed(5)
+    x = torch.rand(B, T, D, generator=g).to(dev)
+    y = torch.rand(B, 1, generator=g).to(dev)
+    out = []
+    for mode in ('0', '1'):
+        monkeypatch.setenv('ADMM_ATR_WIDE', mode)
+        torch.manual_seed(0)
+        m = LSTM(D, H, 1).to(dev)
+        opt = admm.ADMMBasedOptimizer(m, (x, y), example_parameter_dictionary['GoogleStock'], verbose=False)
+        for _ in range(4):
+            opt.step()
+        out.append((torch.cat([p.detach().flatten() for p in m.parameters()]),
+                    torch.cat([v.flatten() for v in opt.gates.values()] + [v.flatten() for v in opt.duals.values()])))
+        del opt
+    assert torch.isfinite(out[1][0]).all() and torch.isfinite(out[1][1]).all()
+    assert torch.equal(out[0][0], out[1][0])
+    assert torch.equal(out[0][1], out[1][1])
+
+
 @pytest.mark.parametrize('shape,D_', [((300, 3, 256), 16), ((257, 4, 256), 5), ((130, 3, 512), 1)])
 def test_speculative_x_update_bit_identical(shape, D_, mods, dev, monkeypatch):
     """SpecX (H % 256 == 0): pass 0 of the x-side trials writes z + x dWx for last step's

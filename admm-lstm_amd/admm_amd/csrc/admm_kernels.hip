@@ -293,6 +293,9 @@ __device__ unsigned long long g_cs_t[64][12];
 #endif
 
 constexpr int SR_ROWS = 32, SR_THREADS = 512;
+#ifndef SR16_PRO_ORDER
+#define SR16_PRO_ORDER 1   // 0: the 16-row producer's B-ring prologue in the scheduler's order (A/B builds)
+#endif
 #ifdef SR_TIMING
 __device__ unsigned long long g_sr_wait[2048][2];   // per workgroup: cycles the producer / consumer wave 0 waited at barriers
 #define SR_SYNC() do { const unsigned long long t0_ = clock64(); __syncthreads(); \
@@ -511,11 +514,16 @@ __global__ __launch_bounds__(SR_THREADS) void k_sweep_rows(Geom g, const bf16x8*
     const bf16x8* wq = wt + (size_t)q * GT * 12 * 64 + lane;
     bf16x8 bq[U][4][3];
 #pragma unroll
-    for (int u = 0; u < U; ++u)
+    for (int u = 0; u < U; ++u) {
 #pragma unroll
       for (int j = 0; j < 4; ++j)
 #pragma unroll
         for (int p = 0; p < 3; ++p) bq[u][j][p] = wq[(u * 12 + j * 3 + p) * 64];
+      // in slot order, as the loop refills them: the loop's vmcnt waits are merged over its entry
+      // and its back edge, and a prologue scheduled slot 1 before slot 0 made every slot-0 chunk
+      // wait for all loads in flight (vmcnt(0)), i.e. the ring one chunk deep instead of U
+      if (SR16_PRO_ORDER) __builtin_amdgcn_sched_barrier(0);
+    }
     f32x4 acc[4] = {};
     for (int t = 1; t <= T; ++t) {
       const __bf16* A = &Ab[t & 1][r16 * AST + 8 * kq];

@@ -293,6 +293,9 @@ __device__ unsigned long long g_cs_t[64][12];
 #endif
 
 constexpr int SR_ROWS = 32, SR_THREADS = 512;
+#ifndef SR_CS_ORDER
+#define SR_CS_ORDER 1   // 0: the column split's producer ring as before round 6's fix (A/B builds)
+#endif
 #ifndef SR16_PRO_ORDER
 #define SR16_PRO_ORDER 1   // 0: the 16-row producer's B-ring prologue in the scheduler's order (A/B builds)
 #endif
@@ -580,9 +583,11 @@ __global__ __launch_bounds__(SR_THREADS) void k_sweep_rows(Geom g, const bf16x8*
     bf16x8 bq[NTC == 1 ? 1 : U][3];
     if constexpr (NTC > 1) {
 #pragma unroll
-      for (int u = 0; u < U; ++u)
+      for (int u = 0; u < U; ++u) {
 #pragma unroll
         for (int p = 0; p < 3; ++p) bq[u][p] = wq[(u * 3 + p) * 64];
+        if (SR_CS_ORDER) __builtin_amdgcn_sched_barrier(0);   // in slot order (see the 16-row producer)
+      }
     }
     f32x16 acc = {};
     f32x4 gx[NTC][2];
@@ -679,12 +684,13 @@ __global__ __launch_bounds__(SR_THREADS) void k_sweep_rows(Geom g, const bf16x8*
       }
     } else {
     const int total = T * GTC;
-#pragma unroll 1
-    for (int G0 = 0; G0 < total; G0 += U) {
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const int G = G0 + u;
-        if (G < total) {
+    // chunk G through ring slot u.  The loop runs whole groups of U chunks with no per-chunk guard
+    // (SR_CS_ORDER): with one, the path on which slot u - 1 was skipped reaches slot u's waits, and
+    // the loop's vmcnt waits merged over it drained every load in flight (vmcnt(0)) in every slot
+    auto chunk = [&](auto uc, const int G) {
+      constexpr int u = decltype(uc)::value;
+      {
+        {
           const int t = G / GTC + 1, r = G - (t - 1) * GTC, nl = r / KC2, cc = r - nl * KC2;
           if (nl == 0 && cc == 0 && q == 0) CS_STAMP(t, 8);
           if (nl == 0 && cc == XC) SR_SYNC();   // mid-step: all of h_{t-1} is in this A buffer
@@ -715,7 +721,25 @@ __global__ __launch_bounds__(SR_THREADS) void k_sweep_rows(Geom g, const bf16x8*
           }
         }
       }
+    };
+    int G0 = 0;
+    if (SR_CS_ORDER) {
+#pragma unroll 1
+      for (; G0 + U <= total; G0 += U) {
+        chunk(std::integral_constant<int, 0>{}, G0);
+        chunk(std::integral_constant<int, 1>{}, G0 + 1);
+        chunk(std::integral_constant<int, 2>{}, G0 + 2);
+        chunk(std::integral_constant<int, 3>{}, G0 + 3);
+      }
     }
+#pragma unroll 1
+    for (; G0 < total; G0 += U) {
+      chunk(std::integral_constant<int, 0>{}, G0);
+      if (G0 + 1 < total) chunk(std::integral_constant<int, 1>{}, G0 + 1);
+      if (G0 + 2 < total) chunk(std::integral_constant<int, 2>{}, G0 + 2);
+      if (G0 + 3 < total) chunk(std::integral_constant<int, 3>{}, G0 + 3);
+    }
+    static_assert(U == 4, "the chunk calls above spell out four ring slots");
     }   // NTC > 1
     __syncthreads();         // final step: the consumer drains the last tile
     if constexpr (GX) {
